@@ -1,0 +1,98 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  Never linked into, loaded by, or called
+ * from the product path (simd-ray-tracer_amd/).  Only tests/, bench.py's
+ * cpu_baseline leg and __graft_entry__.smoke() use it, and only as a checker.
+ *
+ * Plain-C restatement of the trace path of Ne0nWinds/SIMD-Ray-Tracer
+ * (reference @ 2025-01-03, /root/reference):
+ *   - RenderTile        main.cpp:348-495   (lane-4 "SIMD" semantics, x64_math.h)
+ *   - RenderTileScalar  main.cpp:497-640   (scalar semantics)
+ *   - scene generators  main.cpp:53-268
+ *   - camera basis      main.cpp:776-838 (x87 fcos/fsin, x64_math.h:728-746)
+ *   - PCG / RandomFloat base.h:951-997, per-thread seed mixer main.cpp:667-678
+ *
+ * Parity pin: the reference's math layer (base.h + x64_math.h) is compiled
+ * from where it lies into oracle/_ref/refmath (oracle/Makefile) and checked
+ * against these primitives; the end-to-end FNV-1a hashes recorded from the
+ * verbatim reference in SURVEY.md §8(c) are reproduced by tests/
+ * test_oracle_golden.py.  main.cpp itself needs <emscripten/atomic.h>, which
+ * this image lacks, so the full reference is unbuildable here.
+ */
+#ifndef RT_ORACLE_H
+#define RT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Layouts identical to the reference structs (main.cpp:11-26, base.h:357-375). */
+typedef struct or_v3 { float x, y, z, w; } or_v3;                                   /* 16 B */
+typedef struct or_material { or_v3 color; or_v3 emissive; float specular; float ior; float _pad[2]; } or_material; /* 48 B */
+typedef struct or_sphere { or_v3 pos; float radius; float _pad[3]; or_material mat; } or_sphere;               /* 80 B */
+typedef struct or_group { float px[4], py[4], pz[4], r[4]; } or_group;               /* 64 B */
+
+/* Scene description produced by or_scene_builtin (main.cpp:42-51 'scene'). */
+typedef struct or_scene_info {
+    or_v3 look_at;
+    uint32_t use_sky;
+    float default_distance;
+    float default_xangle;
+    float default_yheight;
+    uint32_t n_spheres;
+    uint32_t n_groups;
+    uint32_t n_materials;
+    uint32_t _pad;
+} or_scene_info;
+
+/* camera_info (main.cpp:270-282), image pointers omitted. */
+typedef struct or_camera {
+    or_v3 position, cam_z, cam_x, cam_y, film_center;
+    float film_w, film_h;
+    uint32_t tiles_x, _pad;
+} or_camera;
+
+enum { OR_SEED_STREAM = 0, OR_SEED_PIXEL = 1 };
+
+/* PRNG primitives (base.h:954-989) and the seed mixer (main.cpp:668-675). */
+uint32_t or_pcg(uint64_t *state);
+float    or_random_float(uint64_t *state, float lo, float hi);
+uint64_t or_seed_mix(uint64_t i);
+/* x86 rsqrtss emulation table: 2 exponent parities x 1024 mantissa keys. */
+void     or_set_rsqrt_lut(const float *lut2048);
+float    or_rsqrt(float x);
+void     or_normalize(const float in[3], float out[3]);       /* x64_math.h:234-245 */
+void     or_normalize_fast(const float in[3], float out[3]);  /* x64_math.h:246-257 */
+
+/* Built-in scenes 0 (RGB glass), 1 (floating spheres), 2 (RTWeekend).
+ * Capacity: 482 spheres / 121 groups / 483 materials. */
+int or_scene_builtin(int index, or_sphere *spheres, or_group *groups, or_material *materials, or_scene_info *info);
+
+/* Camera basis for a scene's look-at and the default or user orbit
+ * (main.cpp:730-838).  x87 fcos/fsin as in x64_math.h:728-746. */
+void or_camera_setup(const or_v3 *look_at, float distance, float xangle, float yheight,
+                     uint32_t width, uint32_t height, or_camera *out);
+
+/* Render `frames` progressive frames, PreviousRayCount = prev_count + f.
+ * simd=1 -> RenderTile lane-4 rules, simd=0 -> RenderTileScalar rules.
+ * seed_mode OR_SEED_STREAM: thread t draws from stream_states[t] in tile
+ *   order (deterministic only with threads == 1), exactly the reference.
+ * seed_mode OR_SEED_PIXEL: the RNG is reseeded per (pixel, frame) with
+ *   or_seed_mix((k*H + y)*W + x), k = PreviousRayCount.
+ * Rows [row_begin, row_end) only (tiles clipped); full image when row_end==0.
+ * prev_v4: W*H*4 floats (read+write), cur_rgba: W*H u32 (write). */
+int or_render(const or_group *groups, uint32_t n_groups,
+              const or_sphere *spheres, uint32_t n_spheres,
+              const or_material *materials, uint32_t use_sky,
+              const or_camera *cam, uint32_t width, uint32_t height,
+              uint32_t prev_count, uint32_t frames, uint32_t max_bounce,
+              int simd, int seed_mode, uint32_t threads, uint64_t *stream_states,
+              uint32_t row_begin, uint32_t row_end,
+              float *prev_v4, uint32_t *cur_rgba, uint64_t *rays_out);
+
+uint64_t or_fnv1a64(const void *data, uint64_t nbytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
