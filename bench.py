@@ -1,0 +1,199 @@
+"""bench.py — Mrays/s of the MI355X sphere trace path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "C2"): 1920x1080, 256 spp, 64 spheres
+(first 64 of the reference's Floating Spheres scene, main.cpp:96-167, with
+that scene's default camera), 8 bounces, per-(pixel, frame) PCG seeds.
+One step = one complete 256-spp render of the frame: every pixel's 256
+progressive frames folded into the running mean and the sRGB RGBA8 stored;
+for N > 1 GPUs the frame is dealt out in interleaved 32-row bands (one rank
+per GPU) and gathered to rank 0 over RCCL, then assembled (strong scaling:
+the total work per step is fixed).  Rays = bounce segments counted as the
+reference counts them (main.cpp:390).
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+# MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md, chip table):
+# 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T f32 VALU ops/s (one add/mul/
+# cmp per lane per cycle; FMA is not usable on this path: every op must round
+# separately to match the reference).  HBM3E 8 TB/s.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0
+
+
+def ops_per_segment(n_spheres: int) -> int:
+    """~21 f32 ops per sphere test + ~70 per segment of shading."""
+    return 21 * n_spheres + 70
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--spheres", type=int, default=64)
+    p.add_argument("--bounces", type=int, default=8)
+    p.add_argument("--scalar", action="store_true", help="RenderTileScalar rules instead of RenderTile")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args, n_rays_gpu_step: int):
+    """The oracle (C restatement of RenderTile, lane-4 SSE, pthread 32x32 tile
+    queue) on this host's cores, on a bounded sample of the same workload:
+    the full 1920x1080 frame, 64 spheres, 8 bounces, k spp, k chosen from a
+    1-spp calibration so the sample takes ~--cpu-seconds."""
+    from oracle import oracle as orc
+    threads = orc.cpu_threads()
+    env_cap = os.environ.get("OMP_NUM_THREADS")
+    if env_cap and env_cap.isdigit():
+        threads = min(threads, int(env_cap))
+    o = orc.scene_builtin(1).prefix(args.spheres)
+    W, H = args.width, args.height
+    cam = orc.camera(o, W, H)
+    t = time.perf_counter()
+    _, _, rays1 = orc.render(o, cam, W, H, frames=1, max_bounce=args.bounces, threads=threads, simd=not args.scalar)
+    dt1 = time.perf_counter() - t
+    k = max(1, min(args.spp, int(args.cpu_seconds / max(dt1, 1e-3))))
+    t = time.perf_counter()
+    _, _, rays = orc.render(o, cam, W, H, frames=k, max_bounce=args.bounces, threads=threads, simd=not args.scalar)
+    dt = time.perf_counter() - t
+    return {"value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{W}x{H}, {k} spp (of {args.spp}), {args.spheres} spheres, {args.bounces} bounces, "
+                      f"{rays} rays in {dt:.2f} s on {threads} threads (oracle/rt_oracle.c, lane-4 SSE "
+                      f"RenderTile restatement, pixel seeds)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as graft
+
+    rt = graft.load_package()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H, S, B, N = args.width, args.height, args.spp, args.bounces, args.spheres
+    scene = rt.scene_prefix(rt.scene_builtin(1), N)
+    cam = rt.camera_setup(scene, W, H)
+    dev = rt.Device(local)
+    dev.upload_scene(scene)
+    band_rows = 32
+    rows = [rt.band_local_rows(H, band_rows, world, r) for r in range(world)]
+    maxr = max(rows)
+    cur = torch.zeros(maxr * W, dtype=torch.int32, device="cuda")
+    prev = torch.zeros((maxr * W, 4), dtype=torch.float32, device="cuda")
+    rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gathered = full = None
+    if world > 1 and rank == 0:
+        gathered = [torch.empty_like(cur) for _ in range(world)]
+        full = torch.empty(H * W, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        rays.zero_()
+        if i is not None:
+            ev[i][0].record(stream)
+        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
+                  prev_count=0, frames=S, max_bounce=B, simd=not args.scalar, band_rows=band_rows, band_count=world,
+                  band_index=rank, accum_zero=True, stream=stream.cuda_stream)
+        if i is not None:
+            ev[i][1].record(stream)
+        if world > 1:  # RCCL gather of the band images to rank 0 over xGMI, then assembly
+            dist.gather(cur, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                stacked = torch.cat(gathered)
+                rt.assemble_bands(stacked.data_ptr(), maxr * W * 4, full.data_ptr(), W, H, 4, band_rows, world,
+                                  stream=stream.cuda_stream)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    rays_per_step = torch.tensor([int(rays.item())], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(rays_per_step)
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = float(t[0]), float(t[1])
+    total_rays = int(rays_per_step.item()) * args.steps
+    value = total_rays / elapsed / 1e6
+
+    if rank == 0:
+        rays_local = int(rays.item())  # rank 0's rays per launch
+        ops = rays_local * ops_per_segment(N)
+        achieved = ops / (kern_ms / 1e3) / 1e12
+        fb_bytes = rows[0] * W * (16 + 4)  # accumulation + RGBA8 written once per launch
+        hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
+        line = {
+            "metric": "Mrays/sec at 1920x1080, 256spp, 8 bounces, 64 spheres",
+            "value": round(value, 1),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (first 64 spheres of the reference's Floating Spheres scene, default camera, "
+                    "per-(pixel,frame) PCG seeds)",
+            "config": {"workload": f"C2: {W}x{H}, {S} spp, {N} spheres, {B} bounces, "
+                                   f"{'scalar' if args.scalar else 'SIMD'} rules",
+                       "width": W, "height": H, "spp": S, "spheres": N, "bounces": B,
+                       "parallelism": f"{world} GPU x interleaved 32-row bands" + (" + RCCL gather" if world > 1 else ""),
+                       "rays_per_step": int(rays_per_step.item())},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                         "kernel": "trace_kernel<SIMD>", "kernel_ms": round(kern_ms, 3),
+                         "work_per_launch": f"{rays_local} segments x (21*{N}+70) f32 ops",
+                         "hbm": {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(hbm_achieved / HBM_PEAK_GBS, 6),
+                                 "bytes_per_launch": fb_bytes}},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, total_rays)
+        print(json.dumps(line), flush=True)
+    dev.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,247 @@
+/*
+ * rt_trace.h — C-ABI of the MI355X-native brute-force sphere trace path.
+ *
+ * Drop-in boundary for the per-pixel trace loop of Ne0nWinds/SIMD-Ray-Tracer
+ * (reference @ 2025-01-03).  The reference has no FFI; its path boundary is
+ *   (a) the tile callback launched by WorkQueueStart(RenderTile | RenderTileScalar,
+ *       TilesX*TilesY, ThreadCount)                     main.cpp:851-856, base.h:166-178
+ *       reading the globals CameraInfo, Scenes[SceneIndex], PreviousRayCount,
+ *       ThreadContexts                                   main.cpp:7, 53-54, 289-290
+ *   (b) the app entry points OnInit / OnRender           base.h:163-164, main.cpp:645-859
+ * Every entry point below names the reference interface it replaces.
+ *
+ * Conventions: plain C types, pointers and sizes only.  Functions return 0 on
+ * success or a negative errno-style code (RT_E*).  Calls on one rt_device are
+ * single-threaded; each device owns one HIP stream unless a stream is passed.
+ * Structs marked "byte-compatible" have the reference's exact layout
+ * (offsets asserted in simd-ray-tracer_amd/csrc/rt_host.cpp and tests/).
+ */
+#ifndef RT_TRACE_H
+#define RT_TRACE_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_TRACE_ABI_VERSION 1u
+#define RT_ALIGN16 __attribute__((aligned(16)))
+
+/* Error codes (negative errno values). */
+#define RT_OK 0
+#define RT_EINVAL (-22)  /* bad argument / shape */
+#define RT_ENOMEM (-12)  /* allocation failed */
+#define RT_ENODEV (-19)  /* no HIP device / HIP runtime error */
+#define RT_EBUSY (-16)   /* previous frame still in flight */
+#define RT_EIO (-5)      /* HIP/RCCL error while running */
+
+/* ------------------------------------------------ byte-compatible structs */
+
+/* v3: base.h:357-375 (4 floats, 16-byte aligned, _w padding lane). */
+typedef struct rt_v3 {
+    float x, y, z, _w;
+} RT_ALIGN16 rt_v3;
+
+/* material: main.cpp:11-16 — 48 B. */
+typedef struct rt_material {
+    rt_v3 Color;
+    rt_v3 Emissive;
+    float Specular;
+    float IndexOfRefraction; /* 0 = diffuse/specular, else dielectric */
+} rt_material;
+
+/* scalar_sphere: main.cpp:17-21 — 80 B. */
+typedef struct rt_scalar_sphere {
+    rt_v3 Position;
+    float Radius;
+    rt_material Material;
+} rt_scalar_sphere;
+
+/* sphere_group: main.cpp:23-26 with SIMD_WIDTH = 4 (v3x4 + f32x4) — 64 B. */
+typedef struct rt_sphere_group {
+    float X[4], Y[4], Z[4], Radii[4];
+} RT_ALIGN16 rt_sphere_group;
+
+/* array<T>: main.cpp:28-40 — 16 B. */
+typedef struct rt_array {
+    void *Data;
+    uint32_t Count;
+} rt_array;
+
+/* scene: main.cpp:42-51 — 80 B. */
+typedef struct rt_scene {
+    rt_v3 LookAt;
+    bool UseSkyColor;
+    float DefaultDistanceFromLookAt;
+    float DefaultXAngle;
+    float DefaultYHeight;
+    rt_array ScalarSpheres; /* rt_scalar_sphere[Count] */
+    rt_array SIMDSpheres;   /* rt_sphere_group[Count]  */
+    rt_array Materials;     /* rt_material[Count]      */
+} rt_scene;
+
+/* format / image: base.h:117-136 — 24 B. */
+#define RT_FORMAT_R32B32G32A32_F32 1u
+#define RT_FORMAT_R8G8B8A8_U32 2u
+typedef struct rt_image {
+    void *Data;
+    uint32_t Width, Height;
+    uint32_t Format;
+} rt_image;
+
+/* camera_info: main.cpp:270-282 — 144 B. */
+typedef struct rt_camera_info {
+    rt_v3 CameraPosition;
+    rt_v3 CameraZ;
+    rt_v3 CameraX;
+    rt_v3 CameraY;
+    rt_v3 FilmCenter;
+    float FilmW;
+    float FilmH;
+    uint32_t TilesX;
+    rt_image CurrentImage;  /* RGBA8 u32 per pixel   */
+    rt_image PreviousImage; /* v4 f32 running mean   */
+} rt_camera_info;
+
+/* render_params: base.h:157-161 — 12 B. */
+typedef struct rt_render_params {
+    uint32_t ThreadCount; /* ignored on the GPU (kept for the signature) */
+    bool EnableSIMD;      /* true: RenderTile rules, false: RenderTileScalar rules */
+    uint32_t SceneIndex;
+} rt_render_params;
+
+/* init_params: base.h:152-155 (string8 = {char*, u32}). */
+typedef struct rt_init_params {
+    uint32_t WindowWidth, WindowHeight;
+    const char *WindowTitle;
+    uint32_t WindowTitleSize;
+} rt_init_params;
+
+/* ------------------------------------------------------ host-side inputs */
+
+/* Built-in scenes 0 RGB Glass, 1 Floating Spheres, 2 RTWeekend, generated
+ * exactly as InitRGBSphereScene / InitRandomizedSphereScene /
+ * InitRTWeekendSphereScene (main.cpp:96-268).  The returned scene points at
+ * library-owned static storage (like the reference's static arrays). */
+int rt_scene_builtin(uint32_t index, rt_scene *out);
+
+/* First `n_spheres` spheres of `in` (the BASELINE "N-sphere" synthetic
+ * scenes are prefixes of scene 1): counts become n, ceil(n/4), n+1; the
+ * data pointers are shared. */
+int rt_scene_prefix(const rt_scene *in, uint32_t n_spheres, rt_scene *out);
+
+/* Camera basis + film for an orbit around scene->LookAt, exactly as
+ * OnRender computes it (main.cpp:763-838, x87 fcos/fsin).  Image fields
+ * of `out` are zeroed; the caller fills them. */
+int rt_camera_setup(const rt_scene *scene, float distance_from_look_at, float x_angle, float y_height,
+                    uint32_t width, uint32_t height, rt_camera_info *out);
+
+/* Per-(pixel, frame) seed of the GPU's 'pixel' seed mode: the per-thread
+ * mixer of main.cpp:668-675 applied to i = (k*H + y)*W + x. */
+uint64_t rt_pixel_seed(uint32_t x, uint32_t y, uint32_t frame, uint32_t width, uint32_t height);
+
+/* -------------------------------------------------------- device context */
+
+typedef struct rt_device rt_device;
+
+/* Replaces OnInit's allocation + WorkQueueCreate (main.cpp:658-665). */
+int rt_device_create(int hip_device, rt_device **out);
+int rt_device_destroy(rt_device *dev);
+
+/* x86 rsqrtss reproduction table (2 x 1024 f32): makes
+ * v3::NormalizeFast (x64_math.h:246-257) bit-exact on the GPU. Required. */
+int rt_set_rsqrt_table(rt_device *dev, const float table[2048]);
+
+/* The built-in table: rsqrtss as captured on an Intel host (the parity
+ * target; tests/golden/rsqrt_lut_intel.bin). */
+int rt_rsqrt_table_builtin(float table_out[2048]);
+
+/* Captures this host CPU's own rsqrtss into a table (x86 only).  Returns
+ * RT_EINVAL when the host's rsqrtss is not representable by a parity +
+ * 10-bit table (checked on a sample of inputs). */
+int rt_rsqrt_table_capture_host(float table_out[2048]);
+
+/* Uploads Scenes[SceneIndex] (read by RenderTile at main.cpp:370) into
+ * HBM: SIMDSpheres/Materials for the SIMD rules, ScalarSpheres for the
+ * scalar rules.  The scene is copied; the caller keeps ownership. */
+int rt_scene_upload(rt_device *dev, const rt_scene *scene);
+
+/* --------------------------------------------------------------- tracing */
+
+#define RT_SEED_PIXEL 1u        /* per-(pixel, frame) PCG seed (GPU parity mode) */
+#define RT_FLAG_ACCUM_ZERO 1u   /* PreviousImage treated as all-zero (not read) */
+
+typedef struct rt_trace_desc {
+    uint32_t Width, Height;   /* full image (CurrentImage.Width/Height)          */
+    uint32_t PreviousRayCount;/* frames already folded into PreviousImage (main.cpp:7) */
+    uint32_t Frames;          /* progressive frames (samples/pixel) to fold now  */
+    uint32_t MaxBounce;       /* the reference literal is 5 (main.cpp:387)       */
+    uint32_t EnableSIMD;      /* 1 RenderTile rules, 0 RenderTileScalar rules    */
+    uint32_t SeedMode;        /* RT_SEED_PIXEL                                   */
+    uint32_t BandRows;        /* row-band height for multi-GPU dispatch (32)     */
+    uint32_t BandCount;       /* bands are dealt round-robin over BandCount GPUs */
+    uint32_t BandIndex;       /* this GPU's residue                              */
+    uint32_t Flags;           /* RT_FLAG_*                                       */
+} rt_trace_desc;
+
+/* Number of image rows owned by band residue `band_index` (the compact
+ * per-GPU framebuffer height). */
+uint32_t rt_band_local_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, uint32_t band_index);
+
+/* Replaces WorkQueueStart(RenderTile|RenderTileScalar, TilesX*TilesY, N)
+ * (main.cpp:851-856) for `Frames` consecutive frames: traces every pixel
+ * of this GPU's bands, folds each frame into the running mean and stores
+ * the sRGB RGBA8 of the last one.  cam->CurrentImage.Data and
+ * cam->PreviousImage.Data are DEVICE pointers to compact band-local images
+ * (rt_band_local_rows x Width).  `d_rays` (device u64) is incremented by
+ * the bounce segments traced (RaysCastInThread, main.cpp:390).
+ * Asynchronous on `stream` (hipStream_t; NULL = the HIP null stream). */
+int rt_trace(rt_device *dev, const rt_camera_info *cam, const rt_trace_desc *desc,
+             uint64_t *d_rays, void *stream);
+
+/* Multi-GPU gather helper: scatters `band_count` compact band images
+ * (device, `elem_bytes` per pixel; rank r's image starts at byte
+ * r * rank_stride_bytes of `d_compact`, as an RCCL gather of padded
+ * per-rank buffers lays them out) into the full image `d_dst` (device). */
+int rt_assemble_bands(const void *d_compact, uint64_t rank_stride_bytes, void *d_dst, uint32_t width,
+                      uint32_t height, uint32_t elem_bytes, uint32_t band_rows, uint32_t band_count,
+                      void *stream);
+
+int rt_device_synchronize(rt_device *dev);
+const char *rt_last_error(void);
+
+/* ----------------------------------------------- OnInit / OnRender driver */
+
+/* OnInit (main.cpp:645-679): window defaults, built-in scenes, device. */
+int rt_on_init(rt_init_params *params);
+
+/* Input state for the orbit camera (the reference polls IsDown(key) at
+ * main.cpp:732-761).  Bits: */
+#define RT_KEY_FORWARD 0x01u  /* W / ArrowUp    */
+#define RT_KEY_BACK 0x02u     /* S / ArrowDown  */
+#define RT_KEY_RIGHT 0x04u    /* D / ArrowRight */
+#define RT_KEY_LEFT 0x08u     /* A / ArrowLeft  */
+#define RT_KEY_UP 0x10u       /* Space          */
+#define RT_KEY_DOWN 0x20u     /* C / LeftControl*/
+#define RT_KEY_RESET 0x40u    /* R              */
+
+/* OnRender (main.cpp:705-859) with the accumulation resident in HBM: one
+ * progressive frame per call, one-frame output lag, reset on
+ * move/resize/scene change/R.  `image` is a HOST RGBA8 image.  Returns 1
+ * when `image` received a completed frame, 0 when not (previous frame
+ * still running), negative on error. */
+int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
+                 uint64_t *out_total_rays_cast, double *out_time_elapsed_ms);
+
+/* Blocks until the in-flight frame (if any) has completed
+ * (WorkQueueWaitUntilCompletion, base.h:175). */
+int rt_on_render_wait(void);
+int rt_on_shutdown(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_TRACE_H */

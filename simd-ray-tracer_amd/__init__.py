@@ -1,0 +1,304 @@
+"""simd_ray_tracer_amd — Python mirror of the reference trace path's interface.
+
+Thin ctypes layer over the in-tree C-ABI library ``librt_trace.so`` (HIP
+kernels for gfx950 + C++ host, see ``include/rt_trace.h``).  It mirrors the
+reference's names and argument meaning:
+
+* ``scene_builtin`` / ``scene_prefix``  — Scenes[] of main.cpp:93-268
+* ``camera_setup``                      — the camera block of OnRender, main.cpp:776-838
+* ``Device.trace``                      — WorkQueueStart(RenderTile|RenderTileScalar, ...), main.cpp:851-856
+* ``on_init`` / ``on_render``           — OnInit / OnRender, base.h:163-164
+
+The library is REQUIRED: every entry point raises if it is missing or if no
+HIP device is present.  There is no CPU fallback on this path (the CPU
+restatement under ``oracle/`` is test infrastructure, never imported here).
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+from ctypes import POINTER, c_bool, c_char_p, c_double, c_float, c_int, c_uint32, c_uint64, c_void_p
+from typing import Optional
+
+import numpy as np
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "librt_trace.so"
+
+RT_SEED_PIXEL = 1
+RT_FLAG_ACCUM_ZERO = 1
+RT_FORMAT_R32B32G32A32_F32 = 1
+RT_FORMAT_R8G8B8A8_U32 = 2
+KEY_FORWARD, KEY_BACK, KEY_RIGHT, KEY_LEFT, KEY_UP, KEY_DOWN, KEY_RESET = (1, 2, 4, 8, 16, 32, 64)
+
+
+# ----------------------------------------------------------- C structs
+class RtV3(ctypes.Structure):
+    _fields_ = [("x", c_float), ("y", c_float), ("z", c_float), ("_w", c_float)]
+
+
+class RtMaterial(ctypes.Structure):  # main.cpp:11-16, 48 B (16-byte aligned in C)
+    _fields_ = [("Color", RtV3), ("Emissive", RtV3), ("Specular", c_float), ("IndexOfRefraction", c_float),
+                ("_pad", c_float * 2)]
+
+
+class RtScalarSphere(ctypes.Structure):  # main.cpp:17-21, 80 B
+    _fields_ = [("Position", RtV3), ("Radius", c_float), ("_pad", c_float * 3), ("Material", RtMaterial)]
+
+
+class RtSphereGroup(ctypes.Structure):  # main.cpp:23-26, 64 B
+    _fields_ = [("X", c_float * 4), ("Y", c_float * 4), ("Z", c_float * 4), ("Radii", c_float * 4)]
+
+
+class RtArray(ctypes.Structure):  # main.cpp:28-40
+    _fields_ = [("Data", c_void_p), ("Count", c_uint32)]
+
+
+class RtScene(ctypes.Structure):  # main.cpp:42-51, 80 B
+    _fields_ = [("LookAt", RtV3), ("UseSkyColor", c_bool), ("DefaultDistanceFromLookAt", c_float),
+                ("DefaultXAngle", c_float), ("DefaultYHeight", c_float), ("ScalarSpheres", RtArray),
+                ("SIMDSpheres", RtArray), ("Materials", RtArray)]
+
+
+class RtImage(ctypes.Structure):  # base.h:132-136
+    _fields_ = [("Data", c_void_p), ("Width", c_uint32), ("Height", c_uint32), ("Format", c_uint32)]
+
+
+class RtCameraInfo(ctypes.Structure):  # main.cpp:270-282, 144 B
+    _fields_ = [("CameraPosition", RtV3), ("CameraZ", RtV3), ("CameraX", RtV3), ("CameraY", RtV3),
+                ("FilmCenter", RtV3), ("FilmW", c_float), ("FilmH", c_float), ("TilesX", c_uint32),
+                ("CurrentImage", RtImage), ("PreviousImage", RtImage)]
+
+
+class RtRenderParams(ctypes.Structure):  # base.h:157-161
+    _fields_ = [("ThreadCount", c_uint32), ("EnableSIMD", c_bool), ("SceneIndex", c_uint32)]
+
+
+class RtInitParams(ctypes.Structure):  # base.h:152-155
+    _fields_ = [("WindowWidth", c_uint32), ("WindowHeight", c_uint32), ("WindowTitle", c_char_p),
+                ("WindowTitleSize", c_uint32)]
+
+
+class RtTraceDesc(ctypes.Structure):
+    _fields_ = [(n, c_uint32) for n in ("Width", "Height", "PreviousRayCount", "Frames", "MaxBounce", "EnableSIMD",
+                                        "SeedMode", "BandRows", "BandCount", "BandIndex", "Flags")]
+
+
+for _t, _n in ((RtV3, 16), (RtMaterial, 48), (RtScalarSphere, 80), (RtSphereGroup, 64), (RtArray, 16),
+               (RtScene, 80), (RtImage, 24), (RtCameraInfo, 144), (RtRenderParams, 12)):
+    assert ctypes.sizeof(_t) == _n, (_t.__name__, ctypes.sizeof(_t), _n)
+
+# Every symbol include/rt_trace.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    "rt_scene_builtin": (c_int, [c_uint32, POINTER(RtScene)]),
+    "rt_scene_prefix": (c_int, [POINTER(RtScene), c_uint32, POINTER(RtScene)]),
+    "rt_camera_setup": (c_int, [POINTER(RtScene), c_float, c_float, c_float, c_uint32, c_uint32,
+                                POINTER(RtCameraInfo)]),
+    "rt_pixel_seed": (c_uint64, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
+    "rt_device_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "rt_device_destroy": (c_int, [c_void_p]),
+    "rt_set_rsqrt_table": (c_int, [c_void_p, c_void_p]),
+    "rt_rsqrt_table_builtin": (c_int, [c_void_p]),
+    "rt_rsqrt_table_capture_host": (c_int, [c_void_p]),
+    "rt_scene_upload": (c_int, [c_void_p, POINTER(RtScene)]),
+    "rt_band_local_rows": (c_uint32, [c_uint32, c_uint32, c_uint32, c_uint32]),
+    "rt_trace": (c_int, [c_void_p, POINTER(RtCameraInfo), POINTER(RtTraceDesc), c_void_p, c_void_p]),
+    "rt_assemble_bands": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
+                                  c_void_p]),
+    "rt_device_synchronize": (c_int, [c_void_p]),
+    "rt_last_error": (c_char_p, []),
+    "rt_on_init": (c_int, [POINTER(RtInitParams)]),
+    "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
+    "rt_on_render_wait": (c_int, []),
+    "rt_on_shutdown": (c_int, []),
+}
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+class RtError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Loads librt_trace.so (built by __graft_entry__.build()); raises if absent."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RtError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        try:  # share torch's HIP runtime when torch is present: its libamdhip64 carries the
+            import torch  # noqa: F401  same soname, so loading it first keeps ONE runtime per process
+        except ImportError:
+            pass
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _check(rc: int, what: str) -> None:
+    if rc < 0:
+        msg = lib().rt_last_error()
+        raise RtError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+# ------------------------------------------------------- host-side inputs
+def scene_builtin(index: int) -> RtScene:
+    s = RtScene()
+    _check(lib().rt_scene_builtin(index, ctypes.byref(s)), "rt_scene_builtin")
+    return s
+
+
+def scene_prefix(scene: RtScene, n_spheres: int) -> RtScene:
+    out = RtScene()
+    _check(lib().rt_scene_prefix(ctypes.byref(scene), n_spheres, ctypes.byref(out)), "rt_scene_prefix")
+    out._keep = getattr(scene, "_keep", None)
+    return out
+
+
+def scene_from_spheres(spheres: np.ndarray, look_at=(0.0, 0.0, 0.0), use_sky: bool = False,
+                       distance: float = 1.0, x_angle: float = 0.0, y_height: float = 0.0) -> RtScene:
+    """Scene from an (N, 20) f32 array of scalar_sphere records (main.cpp:17-21),
+    converted to SIMD groups as ConvertScalarSpheresToSIMDSpheres does (main.cpp:73-91)."""
+    sp = np.ascontiguousarray(spheres, dtype=np.float32).reshape(-1, 20)
+    n = sp.shape[0]
+    ng = (n + 3) // 4
+    groups = np.zeros((ng, 16), np.float32)
+    mats = np.zeros((n + 1, 12), np.float32)
+    for i in range(n):
+        g, l = divmod(i, 4)
+        groups[g, l], groups[g, 4 + l], groups[g, 8 + l], groups[g, 12 + l] = sp[i, 0], sp[i, 1], sp[i, 2], sp[i, 4]
+        mats[i] = sp[i, 8:20]
+    s = RtScene()
+    s.LookAt = RtV3(*look_at, 0.0)
+    s.UseSkyColor = bool(use_sky)
+    s.DefaultDistanceFromLookAt = distance
+    s.DefaultXAngle = x_angle
+    s.DefaultYHeight = y_height
+    s.ScalarSpheres = RtArray(sp.ctypes.data, n)
+    s.SIMDSpheres = RtArray(groups.ctypes.data, ng)
+    s.Materials = RtArray(mats.ctypes.data, n + 1)
+    s._keep = (sp, groups, mats)
+    return s
+
+
+def scene_arrays(scene: RtScene):
+    """(spheres (N,20), groups (G,16), materials (M,12)) f32 copies of a scene."""
+    def arr(a: RtArray, width: int):
+        buf = (ctypes.c_float * (a.Count * width)).from_address(a.Data)
+        return np.frombuffer(buf, dtype=np.float32).reshape(a.Count, width).copy()
+    return arr(scene.ScalarSpheres, 20), arr(scene.SIMDSpheres, 16), arr(scene.Materials, 12)
+
+
+def camera_setup(scene: RtScene, width: int, height: int, distance: Optional[float] = None,
+                 x_angle: Optional[float] = None, y_height: Optional[float] = None) -> RtCameraInfo:
+    cam = RtCameraInfo()
+    d = scene.DefaultDistanceFromLookAt if distance is None else distance
+    a = scene.DefaultXAngle if x_angle is None else x_angle
+    h = scene.DefaultYHeight if y_height is None else y_height
+    _check(lib().rt_camera_setup(ctypes.byref(scene), d, a, h, width, height, ctypes.byref(cam)), "rt_camera_setup")
+    return cam
+
+
+def camera_floats(cam: RtCameraInfo) -> np.ndarray:
+    """The 24-float camera record the oracle consumes (position, Z, X, Y, film centre, W, H, tiles)."""
+    raw = np.frombuffer(ctypes.string_at(ctypes.addressof(cam), 96), dtype=np.float32).copy()
+    return raw
+
+
+def pixel_seed(x: int, y: int, frame: int, width: int, height: int) -> int:
+    return int(lib().rt_pixel_seed(x, y, frame, width, height))
+
+
+def band_local_rows(height: int, band_rows: int, band_count: int, band_index: int) -> int:
+    return int(lib().rt_band_local_rows(height, band_rows, band_count, band_index))
+
+
+def rsqrt_table_builtin() -> np.ndarray:
+    t = np.zeros(2048, np.float32)
+    _check(lib().rt_rsqrt_table_builtin(t.ctypes.data), "rt_rsqrt_table_builtin")
+    return t
+
+
+# ---------------------------------------------------------------- device
+class Device:
+    """One GPU: rsqrt table, uploaded scene, trace launches (rt_device)."""
+
+    def __init__(self, ordinal: int = 0, rsqrt_table: Optional[np.ndarray] = None):
+        h = c_void_p()
+        _check(lib().rt_device_create(ordinal, ctypes.byref(h)), "rt_device_create")
+        self.handle = h
+        table = rsqrt_table_builtin() if rsqrt_table is None else np.ascontiguousarray(rsqrt_table, np.float32)
+        _check(lib().rt_set_rsqrt_table(self.handle, table.ctypes.data), "rt_set_rsqrt_table")
+        self._scene = None
+
+    def upload_scene(self, scene: RtScene) -> None:
+        _check(lib().rt_scene_upload(self.handle, ctypes.byref(scene)), "rt_scene_upload")
+        self._scene = scene
+
+    def trace(self, cam: RtCameraInfo, *, width: int, height: int, prev_ptr: int, cur_ptr: int, rays_ptr: int,
+              prev_count: int = 0, frames: int = 1, max_bounce: int = 5, simd: bool = True,
+              band_rows: int = 32, band_count: int = 1, band_index: int = 0, accum_zero: bool = False,
+              stream: Optional[int] = None) -> None:
+        """Traces `frames` progressive frames into device images (raw device pointers)
+        on the HIP stream handle `stream` (None/0 = the null stream)."""
+        c = RtCameraInfo()
+        ctypes.pointer(c)[0] = cam
+        c.CurrentImage = RtImage(cur_ptr, width, height, RT_FORMAT_R8G8B8A8_U32)
+        c.PreviousImage = RtImage(prev_ptr, width, height, RT_FORMAT_R32B32G32A32_F32)
+        d = RtTraceDesc(width, height, prev_count, frames, max_bounce, 1 if simd else 0, RT_SEED_PIXEL,
+                        band_rows, band_count, band_index, RT_FLAG_ACCUM_ZERO if accum_zero else 0)
+        _check(lib().rt_trace(self.handle, ctypes.byref(c), ctypes.byref(d), c_void_p(rays_ptr),
+                              c_void_p(stream or 0)), "rt_trace")
+
+    def synchronize(self) -> None:
+        _check(lib().rt_device_synchronize(self.handle), "rt_device_synchronize")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().rt_device_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def assemble_bands(compact_ptr: int, rank_stride_bytes: int, dst_ptr: int, width: int, height: int,
+                   elem_bytes: int, band_rows: int, band_count: int, stream: Optional[int] = None) -> None:
+    _check(lib().rt_assemble_bands(c_void_p(compact_ptr), rank_stride_bytes, c_void_p(dst_ptr), width, height,
+                                   elem_bytes, band_rows, band_count, c_void_p(stream or 0)),
+           "rt_assemble_bands")
+
+
+# ------------------------------------------------- OnInit / OnRender mirror
+def on_init() -> RtInitParams:
+    p = RtInitParams()
+    _check(lib().rt_on_init(ctypes.byref(p)), "rt_on_init")
+    return p
+
+
+def on_render(image: np.ndarray, scene_index: int, enable_simd: bool = True, keys: int = 0):
+    """OnRender(Image, RenderParams, &Rays, &Time): `image` is an (H, W) uint32
+    RGBA8 host array.  Returns (completed, total_rays_cast, time_elapsed_ms)."""
+    assert image.dtype == np.uint32 and image.ndim == 2 and image.flags.c_contiguous
+    img = RtImage(image.ctypes.data, image.shape[1], image.shape[0], RT_FORMAT_R8G8B8A8_U32)
+    rays = c_uint64(0)
+    ms = c_double(0.0)
+    rc = lib().rt_on_render(ctypes.byref(img), RtRenderParams(0, enable_simd, scene_index), keys,
+                            ctypes.byref(rays), ctypes.byref(ms))
+    _check(rc, "rt_on_render")
+    return bool(rc), int(rays.value), float(ms.value)
+
+
+def on_render_wait() -> None:
+    _check(lib().rt_on_render_wait(), "rt_on_render_wait")
+
+
+def on_shutdown() -> None:
+    _check(lib().rt_on_shutdown(), "rt_on_shutdown")

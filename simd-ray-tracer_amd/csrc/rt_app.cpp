@@ -1,0 +1,241 @@
+// rt_app.cpp — the OnInit / OnRender frame driver (main.cpp:645-859) with
+// the progressive accumulation resident in HBM, plus the rsqrtss tables.
+//
+// Semantics kept from the reference:
+//   - one progressive frame per OnRender call, launched asynchronously;
+//   - the image handed back is the previously COMPLETED frame (one-frame lag,
+//     main.cpp:783-789), and OnRender returns false while a frame is in flight;
+//   - a scene switch, a camera move, a resize or R resets the running mean
+//     (PreviousRayCount = 0, buffers zeroed; main.cpp:791-804);
+//   - *OutTotalRaysCast = bounce segments of the completed frame,
+//     *OutTimeElapsed = its launch -> completion time (main.cpp:840-849).
+// The reference's WASD/Space/C orbit (main.cpp:730-781) is driven by the
+// RT_KEY_* bits the caller passes instead of the platform's IsDown().
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+#include <string.h>
+
+#include "rt_trace.h"
+
+#include "rsqrt_table_intel.inc"
+
+extern "C" int rt_rsqrt_table_builtin(float out[2048]) {
+    if (!out) return RT_EINVAL;
+    memcpy(out, kRsqrtTableIntelBits, sizeof(kRsqrtTableIntelBits));
+    return RT_OK;
+}
+
+static inline float host_rsqrtss(float x) { return _mm_cvtss_f32(_mm_rsqrt_ss(_mm_set_ss(x))); }
+
+extern "C" int rt_rsqrt_table_capture_host(float out[2048]) {
+    if (!out) return RT_EINVAL;
+    for (uint32_t e = 0; e < 2; ++e)
+        for (uint32_t k = 0; k < 1024; ++k) {
+            uint32_t u = ((127u + e) << 23) | (k << 13);
+            float f;
+            memcpy(&f, &u, 4);
+            out[e * 1024 + k] = host_rsqrtss(f);
+        }
+    // Verify the table model on every mantissa of [1, 4) and a sweep of exponents.
+    for (uint32_t u = 0x3F800000u; u < 0x40800000u; u += 7u) {
+        for (int shift = -14; shift <= 2; shift += 2) {
+            const uint32_t v = u + ((uint32_t)shift << 23);
+            float x;
+            memcpy(&x, &v, 4);
+            const int32_t ex = (int32_t)((v >> 23) & 0xFFu) - 127;
+            const uint32_t par = (uint32_t)ex & 1u;
+            uint32_t base;
+            memcpy(&base, &out[par * 1024u + ((v >> 13) & 1023u)], 4);
+            const uint32_t pred = base - ((uint32_t)((ex - (int32_t)par) >> 1) << 23);
+            const float got = host_rsqrtss(x);
+            uint32_t gb;
+            memcpy(&gb, &got, 4);
+            if (gb != pred) return RT_EINVAL;
+        }
+    }
+    return RT_OK;
+}
+
+namespace {
+
+constexpr float kWorldScale = 0.0625f;
+constexpr float kPi32 = 3.14159265358979323846f;
+
+struct App {
+    bool ready = false;
+    rt_device *dev = nullptr;
+    uint32_t scene_index = 0xFFFFFFFFu;
+    float distance = 0.0f, x_angle = 0.0f, y_height = 0.0f;
+    uint32_t prev_count = 0;
+    uint32_t width = 0, height = 0;
+    void *d_prev = nullptr, *d_cur = nullptr;
+    uint64_t *d_rays = nullptr;
+    hipEvent_t ev_start = nullptr, ev_done = nullptr;
+    hipStream_t stream = nullptr;
+    bool in_flight = false;
+    rt_camera_info cam;
+};
+App g_app;
+
+bool frame_complete() {
+    if (!g_app.in_flight) return true;
+    return hipEventQuery(g_app.ev_done) == hipSuccess;
+}
+
+int wait_frame() {
+    if (!g_app.in_flight) return RT_OK;
+    if (hipEventSynchronize(g_app.ev_done) != hipSuccess) return RT_EIO;
+    return RT_OK;
+}
+
+int copy_current(const rt_image *image) {
+    if (!g_app.d_cur || !image->Data) return RT_OK;
+    const size_t bytes = (size_t)g_app.width * g_app.height * 4u;
+    return hipMemcpy(image->Data, g_app.d_cur, bytes, hipMemcpyDeviceToHost) == hipSuccess ? RT_OK : RT_EIO;
+}
+
+}  // namespace
+
+extern "C" int rt_on_init(rt_init_params *params) {
+    if (params) {  // main.cpp:646-650
+        static const char kTitle[] = "SIMD Ray Tracer";
+        params->WindowTitle = kTitle;
+        params->WindowTitleSize = sizeof(kTitle) - 1u;
+        params->WindowWidth = 1280;
+        params->WindowHeight = 720;
+    }
+    if (g_app.ready) return RT_OK;
+    rt_scene s;
+    int rc = rt_scene_builtin(0, &s);  // builds all three scenes (main.cpp:652-654)
+    if (rc) return rc;
+    rc = rt_device_create(0, &g_app.dev);
+    if (rc) return rc;
+    float table[2048];
+    rt_rsqrt_table_builtin(table);
+    rc = rt_set_rsqrt_table(g_app.dev, table);
+    if (rc) return rc;
+    if (hipMalloc(&g_app.d_rays, sizeof(uint64_t)) != hipSuccess ||
+        hipEventCreate(&g_app.ev_start) != hipSuccess || hipEventCreate(&g_app.ev_done) != hipSuccess ||
+        hipStreamCreateWithFlags(&g_app.stream, hipStreamNonBlocking) != hipSuccess)
+        return RT_ENOMEM;
+    (void)hipMemset(g_app.d_rays, 0, sizeof(uint64_t));
+    g_app.ready = true;
+    return RT_OK;
+}
+
+extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
+                            uint64_t *out_total_rays_cast, double *out_time_elapsed_ms) {
+    if (!g_app.ready || !image || image->Width == 0 || image->Height == 0) return RT_EINVAL;
+    if (params.SceneIndex > 2) return RT_EINVAL;
+    bool moved = false;
+    if (g_app.scene_index != params.SceneIndex) {  // main.cpp:718-727
+        if (!frame_complete()) return 0;
+        rt_scene sc;
+        rt_scene_builtin(params.SceneIndex, &sc);
+        int rc = rt_scene_upload(g_app.dev, &sc);
+        if (rc) return rc;
+        g_app.scene_index = params.SceneIndex;
+        g_app.distance = sc.DefaultDistanceFromLookAt;
+        g_app.x_angle = sc.DefaultXAngle;
+        g_app.y_height = sc.DefaultYHeight;
+        moved = true;
+    }
+    {  // main.cpp:730-775
+        const float speed = 1.0f * kWorldScale;
+        if (keys & RT_KEY_FORWARD) { g_app.distance -= speed; moved = true; }
+        if (keys & RT_KEY_BACK) { g_app.distance += speed; moved = true; }
+        if (keys & RT_KEY_RIGHT) { g_app.x_angle -= 1.0f / 16.0f; moved = true; }
+        if (keys & RT_KEY_LEFT) { g_app.x_angle += 1.0f / 16.0f; moved = true; }
+        if (keys & RT_KEY_UP) { g_app.y_height += speed; moved = true; }
+        if (keys & RT_KEY_DOWN) { g_app.y_height -= speed; moved = true; }
+        if (g_app.x_angle > kPi32 * 2.0f) g_app.x_angle -= kPi32 * 4.0f;
+        if (g_app.x_angle < -(kPi32 * 2.0f)) g_app.x_angle += kPi32 * 4.0f;
+        if (g_app.distance < 0.5f * kWorldScale) g_app.distance = 0.5f * kWorldScale;
+        if (g_app.y_height > g_app.distance) g_app.y_height = g_app.distance;
+    }
+    const bool complete = frame_complete();                                          // :783
+    const bool resize = image->Width != g_app.width || image->Height != g_app.height;  // :784
+    bool copy_out = complete && !resize;
+    if (copy_out && copy_current(image) != RT_OK) return RT_EIO;
+    if (resize || moved || (keys & RT_KEY_RESET)) {  // :791-804
+        if (wait_frame() != RT_OK) return RT_EIO;
+        if (!resize) {
+            if (copy_current(image) != RT_OK) return RT_EIO;
+            copy_out = true;
+        }
+        g_app.prev_count = 0;
+        const size_t px = (size_t)image->Width * image->Height;
+        if (resize) {
+            (void)hipFree(g_app.d_prev);
+            (void)hipFree(g_app.d_cur);
+            g_app.d_prev = g_app.d_cur = nullptr;
+            if (hipMalloc(&g_app.d_prev, px * 16u) != hipSuccess || hipMalloc(&g_app.d_cur, px * 4u) != hipSuccess)
+                return RT_ENOMEM;
+            g_app.width = image->Width;
+            g_app.height = image->Height;
+        }
+        // the arena zero-fills on Push (wasm/wasm.cpp:52)
+        if (hipMemsetAsync(g_app.d_prev, 0, px * 16u, g_app.stream) != hipSuccess ||
+            hipMemsetAsync(g_app.d_cur, 0, px * 4u, g_app.stream) != hipSuccess)
+            return RT_EIO;
+    } else if (complete) {
+        g_app.prev_count += 1;  // :805-806
+    } else {
+        return 0;  // :807-808
+    }
+    rt_scene sc;
+    rt_scene_builtin(g_app.scene_index, &sc);
+    int rc = rt_camera_setup(&sc, g_app.distance, g_app.x_angle, g_app.y_height, g_app.width, g_app.height, &g_app.cam);
+    if (rc) return rc;
+    g_app.cam.CurrentImage.Data = g_app.d_cur;
+    g_app.cam.CurrentImage.Width = g_app.width;
+    g_app.cam.CurrentImage.Height = g_app.height;
+    g_app.cam.CurrentImage.Format = RT_FORMAT_R8G8B8A8_U32;
+    g_app.cam.PreviousImage.Data = g_app.d_prev;
+    g_app.cam.PreviousImage.Width = g_app.width;
+    g_app.cam.PreviousImage.Height = g_app.height;
+    g_app.cam.PreviousImage.Format = RT_FORMAT_R32B32G32A32_F32;
+    if (copy_out && out_total_rays_cast) {  // :840-842
+        if (hipMemcpy(out_total_rays_cast, g_app.d_rays, sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return RT_EIO;
+    }
+    if (out_time_elapsed_ms) {  // :848
+        float ms = 0.0f;
+        if (g_app.in_flight && hipEventElapsedTime(&ms, g_app.ev_start, g_app.ev_done) != hipSuccess) ms = 0.0f;
+        *out_time_elapsed_ms = ms;
+    }
+    if (hipMemsetAsync(g_app.d_rays, 0, sizeof(uint64_t), g_app.stream) != hipSuccess) return RT_EIO;  // :843-846
+    rt_trace_desc desc;
+    memset(&desc, 0, sizeof(desc));
+    desc.Width = g_app.width;
+    desc.Height = g_app.height;
+    desc.PreviousRayCount = g_app.prev_count;
+    desc.Frames = 1;
+    desc.MaxBounce = 5;  // main.cpp:387
+    desc.EnableSIMD = params.EnableSIMD ? 1u : 0u;
+    desc.SeedMode = RT_SEED_PIXEL;
+    desc.BandRows = 32;
+    desc.BandCount = 1;
+    if (hipEventRecord(g_app.ev_start, g_app.stream) != hipSuccess) return RT_EIO;
+    rc = rt_trace(g_app.dev, &g_app.cam, &desc, g_app.d_rays, g_app.stream);
+    if (rc) return rc;
+    if (hipEventRecord(g_app.ev_done, g_app.stream) != hipSuccess) return RT_EIO;
+    g_app.in_flight = true;
+    return copy_out ? 1 : 0;
+}
+
+extern "C" int rt_on_render_wait(void) { return g_app.ready ? wait_frame() : RT_OK; }
+
+extern "C" int rt_on_shutdown(void) {
+    if (!g_app.ready) return RT_OK;
+    wait_frame();
+    (void)hipFree(g_app.d_prev);
+    (void)hipFree(g_app.d_cur);
+    (void)hipFree(g_app.d_rays);
+    (void)hipEventDestroy(g_app.ev_start);
+    (void)hipEventDestroy(g_app.ev_done);
+    (void)hipStreamDestroy(g_app.stream);
+    rt_device_destroy(g_app.dev);
+    g_app = App();
+    return RT_OK;
+}

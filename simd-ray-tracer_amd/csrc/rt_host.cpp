@@ -1,0 +1,247 @@
+// rt_host.cpp — C-ABI host side: device context, scene upload, trace launch,
+// band assembly.  Plain HIP runtime; no torch types cross this boundary.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "rt_kernel.h"
+#include "rt_trace.h"
+
+struct rt_device {
+    int ordinal = 0;
+    hipStream_t stream = nullptr;
+    float *d_lut = nullptr;                // 2048 f32
+    bool lut_set = false;
+    // SIMD rule set (SIMDSpheres + Materials) and scalar rule set (ScalarSpheres)
+    float4 *d_groups[2] = {nullptr, nullptr};
+    float4 *d_mats[2] = {nullptr, nullptr};
+    uint32_t n_groups[2] = {0, 0};
+    uint32_t n_spheres = 0;
+    size_t cap_groups[2] = {0, 0};
+    bool scene_set = false;
+    bool use_sky = false;
+    int src = kSrcSmem;
+};
+
+static thread_local char g_err[512];
+
+static int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_OK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(RT_EIO, "%s: %s", #expr, hipGetErrorString(e_));   \
+    } while (0)
+
+extern "C" const char *rt_last_error(void) { return g_err; }
+
+extern "C" int rt_device_create(int hip_device, rt_device **out) {
+    if (!out) return fail(RT_EINVAL, "rt_device_create: out is NULL");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(RT_ENODEV, "rt_device_create: no HIP device visible");
+    if (hip_device < 0 || hip_device >= count) return fail(RT_EINVAL, "rt_device_create: bad device %d", hip_device);
+    HIP_OK(hipSetDevice(hip_device));
+    rt_device *d = new rt_device();
+    d->ordinal = hip_device;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&d->d_lut, 2048 * sizeof(float)) != hipSuccess) {
+        delete d;
+        return fail(RT_ENOMEM, "rt_device_create: stream/LUT allocation failed");
+    }
+    const char *src = getenv("RT_SPHERE_SRC");
+    if (src && strcmp(src, "lds") == 0) d->src = kSrcLds;
+    *out = d;
+    return RT_OK;
+}
+
+extern "C" int rt_device_destroy(rt_device *d) {
+    if (!d) return RT_OK;
+    (void)hipSetDevice(d->ordinal);
+    (void)hipStreamSynchronize(d->stream);
+    for (int r = 0; r < 2; ++r) {
+        (void)hipFree(d->d_groups[r]);
+        (void)hipFree(d->d_mats[r]);
+    }
+    (void)hipFree(d->d_lut);
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+    return RT_OK;
+}
+
+extern "C" int rt_set_rsqrt_table(rt_device *d, const float table[2048]) {
+    if (!d || !table) return fail(RT_EINVAL, "rt_set_rsqrt_table: NULL argument");
+    HIP_OK(hipSetDevice(d->ordinal));
+    HIP_OK(hipMemcpyAsync(d->d_lut, table, 2048 * sizeof(float), hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipStreamSynchronize(d->stream));
+    d->lut_set = true;
+    return RT_OK;
+}
+
+// Packs one rule set: positions/radii as 4-wide groups with r*r precomputed,
+// materials as {Color.xyz, Specular}, {Emissive.xyz, IOR}.
+static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, const std::vector<float> &mats,
+                      uint32_t n_groups) {
+    if (n_groups > d->cap_groups[rs]) {
+        (void)hipFree(d->d_groups[rs]);
+        (void)hipFree(d->d_mats[rs]);
+        d->d_groups[rs] = nullptr;
+        d->d_mats[rs] = nullptr;
+        if (hipMalloc(&d->d_groups[rs], (size_t)n_groups * 64) != hipSuccess ||
+            hipMalloc(&d->d_mats[rs], (size_t)n_groups * 128) != hipSuccess)
+            return fail(RT_ENOMEM, "rt_scene_upload: device allocation failed");
+        d->cap_groups[rs] = n_groups;
+    }
+    HIP_OK(hipMemcpyAsync(d->d_groups[rs], groups.data(), (size_t)n_groups * 64, hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(d->d_mats[rs], mats.data(), (size_t)n_groups * 128, hipMemcpyHostToDevice, d->stream));
+    d->n_groups[rs] = n_groups;
+    return RT_OK;
+}
+
+static void put_material(float *dst, const rt_material &m) {
+    dst[0] = m.Color.x;
+    dst[1] = m.Color.y;
+    dst[2] = m.Color.z;
+    dst[3] = m.Specular;
+    dst[4] = m.Emissive.x;
+    dst[5] = m.Emissive.y;
+    dst[6] = m.Emissive.z;
+    dst[7] = m.IndexOfRefraction;
+}
+
+extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
+    if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
+    const uint32_t ng = scene->SIMDSpheres.Count;
+    const uint32_t ns = scene->ScalarSpheres.Count;
+    if (ng == 0 || !scene->SIMDSpheres.Data || !scene->Materials.Data || ns == 0 || !scene->ScalarSpheres.Data)
+        return fail(RT_EINVAL, "rt_scene_upload: empty scene");
+    const uint32_t ngs = (ns + 3u) / 4u;
+    if (ng > kMaxLdsGroups || ngs > kMaxLdsGroups)
+        return fail(RT_EINVAL, "rt_scene_upload: %u spheres exceed the LDS-staged limit of %u", ns, 4u * kMaxLdsGroups);
+    HIP_OK(hipSetDevice(d->ordinal));
+    // SIMD rules: SIMDSpheres (main.cpp:399-400) + Materials[4g+l] (main.cpp:443-444).
+    {
+        const rt_sphere_group *g = (const rt_sphere_group *)scene->SIMDSpheres.Data;
+        const rt_material *m = (const rt_material *)scene->Materials.Data;
+        std::vector<float> gv((size_t)ng * 16), mv((size_t)ng * 32, 0.0f);
+        for (uint32_t i = 0; i < ng; ++i) {
+            for (int l = 0; l < 4; ++l) {
+                gv[i * 16 + 0 + l] = g[i].X[l];
+                gv[i * 16 + 4 + l] = g[i].Y[l];
+                gv[i * 16 + 8 + l] = g[i].Z[l];
+                gv[i * 16 + 12 + l] = g[i].Radii[l] * g[i].Radii[l];
+                const uint32_t s = 4u * i + (uint32_t)l;
+                if (s < scene->Materials.Count) put_material(&mv[(size_t)s * 8], m[s]);
+            }
+        }
+        int rc = upload_set(d, 0, gv, mv, ng);
+        if (rc) return rc;
+    }
+    // Scalar rules: ScalarSpheres[s].Position/Radius/Material (main.cpp:547-590).
+    {
+        const rt_scalar_sphere *s = (const rt_scalar_sphere *)scene->ScalarSpheres.Data;
+        std::vector<float> gv((size_t)ngs * 16, 0.0f), mv((size_t)ngs * 32, 0.0f);
+        for (uint32_t i = 0; i < ns; ++i) {
+            const uint32_t gi = i / 4u, l = i % 4u;
+            gv[gi * 16 + 0 + l] = s[i].Position.x;
+            gv[gi * 16 + 4 + l] = s[i].Position.y;
+            gv[gi * 16 + 8 + l] = s[i].Position.z;
+            gv[gi * 16 + 12 + l] = s[i].Radius * s[i].Radius;
+            put_material(&mv[(size_t)i * 8], s[i].Material);
+        }
+        // Padding lanes of the scalar packing are skipped by the kernel's
+        // s < n_spheres test (the scalar loop runs to Count, main.cpp:547).
+        for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 16 + 12 + (i % 4u)] = -__builtin_inff();
+        int rc = upload_set(d, 1, gv, mv, ngs);
+        if (rc) return rc;
+    }
+    HIP_OK(hipStreamSynchronize(d->stream));
+    d->n_spheres = ns;
+    d->use_sky = scene->UseSkyColor;
+    d->scene_set = true;
+    return RT_OK;
+}
+
+extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
+                        void *stream) {
+    if (!d || !cam || !desc || !d_rays) return fail(RT_EINVAL, "rt_trace: NULL argument");
+    if (!d->lut_set) return fail(RT_EINVAL, "rt_trace: rsqrt table not set (rt_set_rsqrt_table)");
+    if (!d->scene_set) return fail(RT_EINVAL, "rt_trace: no scene uploaded (rt_scene_upload)");
+    if (desc->SeedMode != RT_SEED_PIXEL) return fail(RT_EINVAL, "rt_trace: only RT_SEED_PIXEL runs on the GPU");
+    if (desc->Width == 0 || desc->Height == 0 || desc->Width > 65536 || desc->Height > 65536)
+        return fail(RT_EINVAL, "rt_trace: bad image size %ux%u", desc->Width, desc->Height);
+    const uint32_t band_rows = desc->BandRows ? desc->BandRows : 32u;
+    const uint32_t band_count = desc->BandCount ? desc->BandCount : 1u;
+    if (desc->BandIndex >= band_count) return fail(RT_EINVAL, "rt_trace: BandIndex >= BandCount");
+    const uint32_t local_rows = rt_band_local_rows(desc->Height, band_rows, band_count, desc->BandIndex);
+    if (desc->Frames == 0 || local_rows == 0) return RT_OK;
+    if (!cam->CurrentImage.Data || !cam->PreviousImage.Data)
+        return fail(RT_EINVAL, "rt_trace: CurrentImage/PreviousImage device pointers missing");
+    const int rs = desc->EnableSIMD ? 0 : 1;
+    TraceArgs a;
+    memset(&a, 0, sizeof(a));
+    a.groups = d->d_groups[rs];
+    a.materials = d->d_mats[rs];
+    a.rsqrt_lut = d->d_lut;
+    a.prev = (float4 *)cam->PreviousImage.Data;
+    a.cur = (uint32_t *)cam->CurrentImage.Data;
+    a.rays = (unsigned long long *)d_rays;
+    const rt_v3 *v[4] = {&cam->CameraPosition, &cam->CameraX, &cam->CameraY, &cam->FilmCenter};
+    float *dst[4] = {a.cam_pos, a.cam_x, a.cam_y, a.film_center};
+    for (int i = 0; i < 4; ++i) {
+        dst[i][0] = v[i]->x;
+        dst[i][1] = v[i]->y;
+        dst[i][2] = v[i]->z;
+    }
+    a.film_w = cam->FilmW;
+    a.film_h = cam->FilmH;
+    a.width = desc->Width;
+    a.height = desc->Height;
+    a.local_rows = local_rows;
+    a.prev_count = desc->PreviousRayCount;
+    a.frames = desc->Frames;
+    a.max_bounce = desc->MaxBounce;
+    a.n_groups = d->n_groups[rs];
+    a.n_spheres = d->n_spheres;
+    a.use_sky = d->use_sky ? 1u : 0u;
+    a.flags = (desc->Flags & RT_FLAG_ACCUM_ZERO) ? kFlagAccumZero : 0u;
+    a.band_rows = band_rows;
+    a.band_count = band_count;
+    a.band_index = desc->BandIndex;
+    HIP_OK(hipSetDevice(d->ordinal));
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
+    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, s) != 0)
+        return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return RT_OK;
+}
+
+extern "C" int rt_assemble_bands(const void *d_compact, uint64_t rank_stride_bytes, void *d_dst, uint32_t width,
+                                 uint32_t height, uint32_t elem_bytes, uint32_t band_rows, uint32_t band_count,
+                                 void *stream) {
+    if (!d_compact || !d_dst || width == 0 || height == 0 || elem_bytes == 0 || band_rows == 0 || band_count == 0)
+        return fail(RT_EINVAL, "rt_assemble_bands: bad argument");
+    for (uint32_t r = 0; r < band_count; ++r)
+        if ((uint64_t)rt_band_local_rows(height, band_rows, band_count, r) * width * elem_bytes > rank_stride_bytes)
+            return fail(RT_EINVAL, "rt_assemble_bands: rank stride too small for rank %u", r);
+    if (rtk_launch_assemble(d_compact, rank_stride_bytes, d_dst, width, height, elem_bytes, band_rows, band_count,
+                            (hipStream_t)stream) != 0)
+        return fail(RT_EIO, "rt_assemble_bands: launch failed");
+    return RT_OK;
+}
+
+extern "C" int rt_device_synchronize(rt_device *d) {
+    if (!d) return fail(RT_EINVAL, "rt_device_synchronize: NULL device");
+    HIP_OK(hipSetDevice(d->ordinal));
+    HIP_OK(hipStreamSynchronize(d->stream));
+    return RT_OK;
+}

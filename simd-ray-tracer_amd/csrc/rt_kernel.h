@@ -1,0 +1,39 @@
+// rt_kernel.h — launch contract between the C-ABI host (rt_host.cpp) and the
+// gfx950 trace kernel (rt_kernel.hip).  Internal; not part of include/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+enum { kSrcSmem = 0, kSrcLds = 1 };  // where the sphere loop reads its groups
+enum { kFlagAccumZero = 1 };
+
+// HBM layout of an uploaded scene (per rule set):
+//   groups    : n_groups x 4 float4 = {x[4]}, {y[4]}, {z[4]}, {r*r[4]}   (64 B/group)
+//   materials : 4*n_groups x 2 float4 = {Color.xyz, Specular}, {Emissive.xyz, IOR} (32 B/sphere)
+// r*r is precomputed on the host with the same f32 multiply the reference
+// repeats per test (main.cpp:406), so it is bit-identical.
+struct TraceArgs {
+    const float4 *groups;
+    const float4 *materials;
+    const float *rsqrt_lut;      // 2048 f32
+    float4 *prev;                // compact band image, local_rows x width
+    uint32_t *cur;               // compact band image, local_rows x width
+    unsigned long long *rays;    // accumulated bounce segments
+    float cam_pos[3], cam_x[3], cam_y[3], film_center[3];
+    float film_w, film_h;
+    uint32_t width, height, local_rows;
+    uint32_t prev_count, frames, max_bounce;
+    uint32_t n_groups, n_spheres, use_sky, flags;  // n_spheres: scalar rule set only
+    uint32_t band_rows, band_count, band_index;
+};
+
+// Dynamic LDS per block: rsqrt table + groups + materials.
+static inline size_t rtk_lds_bytes(uint32_t n_groups) {
+    return 8192u + (size_t)n_groups * 64u + (size_t)n_groups * 128u;
+}
+static const uint32_t kMaxLdsGroups = (65536u - 8192u) / 192u;  // 298 groups = 1192 spheres
+
+extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, hipStream_t stream);
+extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
+                                   uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

@@ -1,0 +1,75 @@
+"""Shared fixtures.  `gpu`-marked tests need a real MI355X (run via gpurun);
+everything else runs on the CPU-only container."""
+import os
+import pathlib
+import sys
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import __graft_entry__ as graft  # noqa: E402
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run on the GPU box")
+
+
+def _ensure_built():
+    lib = ROOT / "simd-ray-tracer_amd" / "librt_trace.so"
+    orc = ROOT / "oracle" / "liboracle.so"
+    if not lib.exists() or not orc.exists():
+        graft.build()
+
+
+@pytest.fixture(scope="session")
+def rt():
+    _ensure_built()
+    pkg = graft.load_package()
+    pkg.lib()
+    return pkg
+
+
+@pytest.fixture(scope="session")
+def orc():
+    _ensure_built()
+    from oracle import oracle as o
+    o.lib()
+    return o
+
+
+@pytest.fixture(scope="session")
+def refmath():
+    """The reference's own math layer (base.h + x64_math.h compiled from
+    /root/reference by oracle/Makefile); only present in the build container."""
+    import ctypes
+    path = ROOT / "oracle" / "_ref" / "librefmath.so"
+    if not path.exists():
+        pytest.skip("oracle/_ref/librefmath.so not built (needs /root/reference)")
+    L = ctypes.CDLL(str(path))
+    f, v, u32, u64p = ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p
+    for name, res, args in [("ref_pcg", u32, [u64p]), ("ref_random_float", f, [u64p, f, f]), ("ref_rsqrt", f, [f]),
+                            ("ref_sqrt", f, [f]), ("ref_min", f, [f, f]), ("ref_normalize", None, [v, v]),
+                            ("ref_normalize_fast", None, [v, v]), ("ref_cross", None, [v, v, v]),
+                            ("ref_dot", f, [v, v]), ("ref_cos", f, [f]), ("ref_sin", f, [f]),
+                            ("ref_horizontal_min", f, [v]), ("ref_group_test", None, [v, v, v, v, v, v, v, v])]:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+@pytest.fixture(scope="session")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch
+
+
+def host_is_intel() -> bool:
+    try:
+        return "GenuineIntel" in pathlib.Path("/proc/cpuinfo").read_text()
+    except OSError:
+        return False
