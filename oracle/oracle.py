@@ -53,6 +53,10 @@ def lib() -> ctypes.CDLL:
                                 c_uint32, c_void_p, c_void_p, c_void_p]
         L.or_fnv1a64.restype = c_uint64
         L.or_fnv1a64.argtypes = [c_void_p, c_uint64]
+        L.or_group_test.argtypes = [c_void_p] * 5
+        L.or_horizontal_min.restype = c_float
+        L.or_horizontal_min.argtypes = [c_void_p, c_void_p]
+        L.or_cross.argtypes = [c_void_p] * 3
         _L = L
         set_lut(np.fromfile(LUT_PATH, dtype=np.float32))
     return _L

@@ -456,13 +456,68 @@ static void sky(const trace_ctx *c, const float dir[3], const float att[3], floa
     }
 }
 
+/* main.cpp:400-407: per group, C = P - O, T = Dot(C, D), |C - D*T|^2, R*R. */
+static inline void group_core(const or_group *sg, __m128 ox, __m128 oy, __m128 oz, __m128 dx, __m128 dy, __m128 dz,
+                              __m128 *cx, __m128 *cy, __m128 *cz, __m128 *t, __m128 *dist, __m128 *r2)
+{
+    *cx = _mm_sub_ps(_mm_loadu_ps(sg->px), ox);
+    *cy = _mm_sub_ps(_mm_loadu_ps(sg->py), oy);
+    *cz = _mm_sub_ps(_mm_loadu_ps(sg->pz), oz);
+    *t = _mm_add_ps(_mm_add_ps(_mm_mul_ps(*cx, dx), _mm_mul_ps(*cy, dy)), _mm_mul_ps(*cz, dz));
+    __m128 qx = _mm_sub_ps(*cx, _mm_mul_ps(dx, *t));
+    __m128 qy = _mm_sub_ps(*cy, _mm_mul_ps(dy, *t));
+    __m128 qz = _mm_sub_ps(*cz, _mm_mul_ps(dz, *t));
+    *dist = _mm_add_ps(_mm_add_ps(_mm_mul_ps(qx, qx), _mm_mul_ps(qy, qy)), _mm_mul_ps(qz, qz));
+    __m128 r = _mm_loadu_ps(sg->r);
+    *r2 = _mm_mul_ps(r, r);
+}
+
+/* main.cpp:413-417: X = sqrt(R^2 - d), t = T - X, or T + X when t < eps. */
+static inline __m128 group_hit_t(__m128 t, __m128 dist, __m128 r2, __m128 *itest)
+{
+    __m128 xx = _mm_sqrt_ps(_mm_sub_ps(r2, dist));
+    __m128 it = _mm_sub_ps(t, xx);
+    *itest = _mm_cmplt_ps(it, _mm_set1_ps(OR_EPS));
+    return _mm_blendv_ps(it, _mm_add_ps(t, xx), *itest);
+}
+
+/* x64_math.h:579-585 HorizontalMin, then the lowest lane holding it
+ * (FindFirstIndex, wasm_math.h:286-291 semantics). */
+static inline uint32_t lane_select(__m128 min_t, float *m_out)
+{
+    __m128 m = _mm_min_ps(min_t, _mm_movehl_ps(min_t, min_t));
+    m = _mm_min_ps(m, _mm_shuffle_ps(m, m, 0x11));
+    float mv = _mm_cvtss_f32(m);
+    *m_out = mv;
+    int mask = _mm_movemask_ps(_mm_cmpeq_ps(min_t, _mm_set1_ps(mv)));
+    return mask ? (uint32_t)__builtin_ctz((unsigned)mask) : 0u;
+}
+
+/* Exported for tests: the lane-4 group arithmetic and selection above. */
+void or_group_test(const float o[3], const float d[3], const or_group *g, float dist_out[4], float t_out[4])
+{
+    __m128 cx, cy, cz, t, dist, r2, itest;
+    group_core(g, _mm_set1_ps(o[0]), _mm_set1_ps(o[1]), _mm_set1_ps(o[2]), _mm_set1_ps(d[0]), _mm_set1_ps(d[1]),
+               _mm_set1_ps(d[2]), &cx, &cy, &cz, &t, &dist, &r2);
+    _mm_storeu_ps(dist_out, dist);
+    _mm_storeu_ps(t_out, group_hit_t(t, dist, r2, &itest));
+}
+
+float or_horizontal_min(const float v[4], uint32_t *lane)
+{
+    float m;
+    *lane = lane_select(_mm_loadu_ps(v), &m);
+    return m;
+}
+
+void or_cross(const float a[3], const float b[3], float out[3]) { cross_fma(a, b, out); }
+
 /* One sample with RenderTile lane-4 rules (main.cpp:375-482). */
 static void trace_simd(const trace_ctx *c, uint32_t x, uint32_t y, uint64_t *rng, float out[3], uint64_t *rays)
 {
     float o[3], d[3], att[3] = {1, 1, 1};
     out[0] = out[1] = out[2] = 0.0f;
     primary_ray(c, x, y, rng, o, d);
-    const __m128 eps = _mm_set1_ps(OR_EPS);
     for (uint32_t b = 0; b < c->max_bounce; ++b) {
         *rays += 1;
         __m128 ox = _mm_set1_ps(o[0]), oy = _mm_set1_ps(o[1]), oz = _mm_set1_ps(o[2]);
@@ -472,24 +527,12 @@ static void trace_simd(const trace_ctx *c, uint32_t x, uint32_t y, uint64_t *rng
         __m128i grp = _mm_setzero_si128();
         __m128 inside = _mm_setzero_ps();
         for (uint32_t g = 0; g < c->n_groups; ++g) {
-            const or_group *sg = &c->groups[g];
-            __m128 cx = _mm_sub_ps(_mm_loadu_ps(sg->px), ox);
-            __m128 cy = _mm_sub_ps(_mm_loadu_ps(sg->py), oy);
-            __m128 cz = _mm_sub_ps(_mm_loadu_ps(sg->pz), oz);
-            __m128 t = _mm_add_ps(_mm_add_ps(_mm_mul_ps(cx, dx), _mm_mul_ps(cy, dy)), _mm_mul_ps(cz, dz));
-            __m128 qx = _mm_sub_ps(cx, _mm_mul_ps(dx, t));
-            __m128 qy = _mm_sub_ps(cy, _mm_mul_ps(dy, t));
-            __m128 qz = _mm_sub_ps(cz, _mm_mul_ps(dz, t));
-            __m128 dist = _mm_add_ps(_mm_add_ps(_mm_mul_ps(qx, qx), _mm_mul_ps(qy, qy)), _mm_mul_ps(qz, qz));
-            __m128 r = _mm_loadu_ps(sg->r);
-            __m128 r2 = _mm_mul_ps(r, r);
+            __m128 cx, cy, cz, t, dist, r2;
+            group_core(&c->groups[g], ox, oy, oz, dx, dy, dz, &cx, &cy, &cz, &t, &dist, &r2);
             __m128 hit = _mm_cmplt_ps(dist, r2);
             if (_mm_movemask_ps(hit) == 0) continue;
-            __m128 xx = _mm_sqrt_ps(_mm_sub_ps(r2, dist));
-            __m128 it = _mm_sub_ps(t, xx);
-            __m128 itest = _mm_cmplt_ps(it, eps);
-            it = _mm_blendv_ps(it, _mm_add_ps(t, xx), itest);
-            __m128 mv = _mm_and_ps(_mm_and_ps(_mm_cmplt_ps(it, min_t), _mm_cmpgt_ps(it, eps)), hit);
+            __m128 itest, it = group_hit_t(t, dist, r2, &itest);
+            __m128 mv = _mm_and_ps(_mm_and_ps(_mm_cmplt_ps(it, min_t), _mm_cmpgt_ps(it, _mm_set1_ps(OR_EPS))), hit);
             if (_mm_movemask_ps(mv) == 0) continue;
             __m128 ipx = _mm_mul_ps(dx, it), ipy = _mm_mul_ps(dy, it), ipz = _mm_mul_ps(dz, it);
             inside = _mm_or_ps(inside, _mm_and_ps(itest, mv));                 /* sticky, main.cpp:425 */
@@ -502,15 +545,12 @@ static void trace_simd(const trace_ctx *c, uint32_t x, uint32_t y, uint64_t *rng
             noy = _mm_blendv_ps(noy, _mm_add_ps(oy, ipy), mv);
             noz = _mm_blendv_ps(noz, _mm_add_ps(oz, ipz), mv);
         }
-        /* x64_math.h:579-585 HorizontalMin, then the lowest lane holding it. */
-        __m128 m = _mm_min_ps(min_t, _mm_movehl_ps(min_t, min_t));
-        m = _mm_min_ps(m, _mm_shuffle_ps(m, m, 0x11));
-        float mv = _mm_cvtss_f32(m);
+        float mv;
+        uint32_t lane = lane_select(min_t, &mv);
         if (mv == OR_FMAX) {
             sky(c, d, att, out);
             break;
         }
-        uint32_t lane = (uint32_t)__builtin_ctz((unsigned)_mm_movemask_ps(_mm_cmpeq_ps(min_t, _mm_set1_ps(mv))));
         float lt[4], hx[4], hy[4], hz[4], nx[4], ny[4], nz[4], in4[4];
         uint32_t g4[4];
         _mm_storeu_ps(lt, min_t);

@@ -11,12 +11,14 @@
  *   - camera basis      main.cpp:776-838 (x87 fcos/fsin, x64_math.h:728-746)
  *   - PCG / RandomFloat base.h:951-997, per-thread seed mixer main.cpp:667-678
  *
- * Parity pin: the reference's math layer (base.h + x64_math.h) is compiled
- * from where it lies into oracle/_ref/refmath (oracle/Makefile) and checked
- * against these primitives; the end-to-end FNV-1a hashes recorded from the
- * verbatim reference in SURVEY.md §8(c) are reproduced by tests/
- * test_oracle_golden.py.  main.cpp itself needs <emscripten/atomic.h>, which
- * this image lacks, so the full reference is unbuildable here.
+ * Parity pin: the reference's math layer (base.h + x64_math.h)
+ * is compiled from where it lies into oracle/_ref/librefmath.so (Makefile)
+ * and checked against these primitives; the known-answer values and the
+ * end-to-end bounce-segment counts recorded from the verbatim reference in
+ * SURVEY.md §7/§8(c) are reproduced (tests/test_oracle_reference.py).  The
+ * survey's FNV-1a image hashes are NOT reproduced (their hashing protocol is
+ * not recoverable).  main.cpp itself needs
+ * <emscripten/atomic.h>, absent here, so the full reference is unbuildable.
  */
 #ifndef RT_ORACLE_H
 #define RT_ORACLE_H
@@ -91,6 +93,12 @@ int or_render(const or_group *groups, uint32_t n_groups,
               float *prev_v4, uint32_t *cur_rgba, uint64_t *rays_out);
 
 uint64_t or_fnv1a64(const void *data, uint64_t nbytes);
+
+/* Exposed pieces of the restatement, for differential tests against the
+ * reference's own math layer (oracle/_ref). */
+void  or_group_test(const float o[3], const float d[3], const or_group *g, float dist_out[4], float t_out[4]);
+float or_horizontal_min(const float v[4], uint32_t *lane);
+void  or_cross(const float a[3], const float b[3], float out[3]);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,59 @@
+"""Generates tests/golden/oracle_regression.json: FNV-1a-64 hashes, ray counts
+and a few raw pixels of oracle renders (pixel and stream seed modes) for the
+configurations the parity tests use.  These are REGRESSION vectors of the
+oracle (which is itself pinned to the reference by test_oracle_reference.py),
+committed so the GPU path can be checked against fixed data too.
+
+    python tests/golden/make_golden.py
+"""
+import json
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+from oracle import oracle as orc  # noqa: E402
+
+CASES = [
+    # name, scene, N, W, H, frames, bounces, simd, seed mode
+    ("c1_simd", 1, 4, 256, 256, 1, 1, True, "pixel"),
+    ("c1_scalar", 1, 4, 256, 256, 1, 1, False, "pixel"),
+    ("n64_b8_128x96x8", 1, 64, 128, 96, 8, 8, True, "pixel"),
+    ("n256_b16_64x64x2", 1, 256, 64, 64, 2, 16, True, "pixel"),
+    ("rgb_glass_96x64x4", 0, None, 96, 64, 4, 5, True, "pixel"),
+    ("rtweekend_80x48x2", 2, None, 80, 48, 2, 5, True, "pixel"),
+    ("rtweekend_80x48x2_scalar", 2, None, 80, 48, 2, 5, False, "pixel"),
+    ("ragged_n13_37x23x3", 1, 13, 37, 23, 3, 6, True, "pixel"),
+    ("survey_scene1_stream_256x4", 1, None, 256, 256, 4, 5, True, "stream"),
+    ("survey_n64_pixel_256x4", 1, 64, 256, 256, 4, 8, True, "pixel"),
+]
+
+
+def render_case(scene, n, W, H, frames, bounces, simd, seed):
+    o = orc.scene_builtin(scene)
+    if n is not None:
+        o = o.prefix(n)
+    mode = orc.SEED_PIXEL if seed == "pixel" else orc.SEED_STREAM
+    return orc.render(o, orc.camera(o, W, H), W, H, frames=frames, max_bounce=bounces, simd=simd,
+                      seed_mode=mode, threads=1 if seed == "stream" else orc.cpu_threads())
+
+
+def main():
+    out = {}
+    for name, scene, n, W, H, frames, bounces, simd, seed in CASES:
+        prev, cur, rays = render_case(scene, n, W, H, frames, bounces, simd, seed)
+        mid = (H // 2) * W + W // 2
+        out[name] = {"scene": scene, "spheres": n, "width": W, "height": H, "frames": frames, "bounces": bounces,
+                     "simd": simd, "seed_mode": seed, "rays": rays,
+                     "fnv1a64_rgba8": f"{orc.fnv1a64(cur):016x}", "fnv1a64_v4": f"{orc.fnv1a64(prev):016x}",
+                     "center_rgba8": f"{int(cur[mid]):08x}",
+                     "center_v4_bits": [f"{int(v):08x}" for v in prev[mid].view(np.uint32)]}
+    path = ROOT / "tests" / "golden" / "oracle_regression.json"
+    path.write_text(json.dumps(out, indent=1) + "\n")
+    print(f"wrote {path} ({len(out)} cases)")
+
+
+if __name__ == "__main__":
+    main()
