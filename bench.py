@@ -187,6 +187,9 @@ def main():
                                  "frac": round(hbm_achieved / HBM_PEAK_GBS, 6),
                                  "bytes_per_launch": fb_bytes}},
         }
+        stats = dev.debug_stats()
+        if stats:
+            line["sched_stats"] = stats
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, total_rays)
         print(json.dumps(line), flush=True)

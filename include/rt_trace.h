@@ -211,6 +211,13 @@ int rt_assemble_bands(const void *d_compact, uint64_t rank_stride_bytes, void *d
                       void *stream);
 
 int rt_device_synchronize(rt_device *dev);
+
+/* Scheduling counters accumulated over trace launches when the process runs
+ * with RT_STATS=1: [0] primary wave-iterations, [1] primary lane-segments,
+ * [2] secondary wave-iterations, [3] secondary lane-segments, [4] sphere
+ * groups tested by primary iterations after culling.  Returns 1 when
+ * enabled, 0 when not (out zeroed), negative on error. */
+int rt_debug_stats(rt_device *dev, uint64_t out[8], int reset);
 const char *rt_last_error(void);
 
 /* ----------------------------------------------- OnInit / OnRender driver */

@@ -16,6 +16,7 @@ restatement under ``oracle/`` is test infrastructure, never imported here).
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
 from ctypes import POINTER, c_bool, c_char_p, c_double, c_float, c_int, c_uint32, c_uint64, c_void_p
 from typing import Optional
@@ -23,7 +24,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = _HERE / "librt_trace.so"
+# RT_TRACE_LIB selects an alternative in-tree build (kernel A/B experiments)
+LIB_PATH = _HERE / os.environ.get("RT_TRACE_LIB", "librt_trace.so")
 
 RT_SEED_PIXEL = 1
 RT_FLAG_ACCUM_ZERO = 1
@@ -106,6 +108,7 @@ SIGNATURES = {
     "rt_assemble_bands": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
                                   c_void_p]),
     "rt_device_synchronize": (c_int, [c_void_p]),
+    "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "rt_last_error": (c_char_p, []),
     "rt_on_init": (c_int, [POINTER(RtInitParams)]),
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
@@ -253,6 +256,16 @@ class Device:
                         band_rows, band_count, band_index, RT_FLAG_ACCUM_ZERO if accum_zero else 0)
         _check(lib().rt_trace(self.handle, ctypes.byref(c), ctypes.byref(d), c_void_p(rays_ptr),
                               c_void_p(stream or 0)), "rt_trace")
+
+    def debug_stats(self, reset: bool = True):
+        """RT_STATS=1 scheduling counters (see rt_debug_stats), or None when disabled."""
+        out = np.zeros(8, np.uint64)
+        rc = lib().rt_debug_stats(self.handle, out.ctypes.data, int(reset))
+        _check(rc, "rt_debug_stats")
+        if rc == 0:
+            return None
+        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups"]
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def synchronize(self) -> None:
         _check(lib().rt_device_synchronize(self.handle), "rt_device_synchronize")

@@ -25,6 +25,9 @@ struct rt_device {
     bool scene_set = false;
     bool use_sky = false;
     int src = kSrcSmem;
+    int cull = 1;
+    uint32_t sec_threshold = 16;
+    unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
 };
 
 static thread_local char g_err[512];
@@ -61,6 +64,13 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     }
     const char *src = getenv("RT_SPHERE_SRC");
     if (src && strcmp(src, "lds") == 0) d->src = kSrcLds;
+    const char *cull = getenv("RT_CULL");  // 0: brute-force primary rays too (A/B)
+    if (cull && cull[0] == '0') d->cull = 0;
+    const char *thr = getenv("RT_SEC_THRESHOLD");
+    if (thr) d->sec_threshold = (uint32_t)atoi(thr);
+    const char *st = getenv("RT_STATS");
+    if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatCount * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long));
     *out = d;
     return RT_OK;
 }
@@ -74,6 +84,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
         (void)hipFree(d->d_mats[r]);
     }
     (void)hipFree(d->d_lut);
+    (void)hipFree(d->d_stats);
     (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
@@ -97,11 +108,13 @@ static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, co
         (void)hipFree(d->d_mats[rs]);
         d->d_groups[rs] = nullptr;
         d->d_mats[rs] = nullptr;
-        if (hipMalloc(&d->d_groups[rs], (size_t)n_groups * 64) != hipSuccess ||
+        // +1 padding group: the kernel prefetches group g+1 while testing g
+        if (hipMalloc(&d->d_groups[rs], (size_t)(n_groups + 1) * 64) != hipSuccess ||
             hipMalloc(&d->d_mats[rs], (size_t)n_groups * 128) != hipSuccess)
             return fail(RT_ENOMEM, "rt_scene_upload: device allocation failed");
         d->cap_groups[rs] = n_groups;
     }
+    HIP_OK(hipMemsetAsync(d->d_groups[rs] + 4 * (size_t)n_groups, 0, 64, d->stream));
     HIP_OK(hipMemcpyAsync(d->d_groups[rs], groups.data(), (size_t)n_groups * 64, hipMemcpyHostToDevice, d->stream));
     HIP_OK(hipMemcpyAsync(d->d_mats[rs], mats.data(), (size_t)n_groups * 128, hipMemcpyHostToDevice, d->stream));
     d->n_groups[rs] = n_groups;
@@ -183,6 +196,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     const uint32_t band_rows = desc->BandRows ? desc->BandRows : 32u;
     const uint32_t band_count = desc->BandCount ? desc->BandCount : 1u;
     if (desc->BandIndex >= band_count) return fail(RT_EINVAL, "rt_trace: BandIndex >= BandCount");
+    if (band_rows % 8u) return fail(RT_EINVAL, "rt_trace: BandRows must be a multiple of 8");
     const uint32_t local_rows = rt_band_local_rows(desc->Height, band_rows, band_count, desc->BandIndex);
     if (desc->Frames == 0 || local_rows == 0) return RT_OK;
     if (!cam->CurrentImage.Data || !cam->PreviousImage.Data)
@@ -218,9 +232,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.band_rows = band_rows;
     a.band_count = band_count;
     a.band_index = desc->BandIndex;
+    a.sec_threshold = d->sec_threshold;
+    a.stats = d->d_stats;
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, s) != 0)
+    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return RT_OK;
 }
@@ -244,4 +260,15 @@ extern "C" int rt_device_synchronize(rt_device *d) {
     HIP_OK(hipSetDevice(d->ordinal));
     HIP_OK(hipStreamSynchronize(d->stream));
     return RT_OK;
+}
+
+extern "C" int rt_debug_stats(rt_device *d, uint64_t out[8], int reset) {
+    if (!d || !out) return fail(RT_EINVAL, "rt_debug_stats: NULL argument");
+    memset(out, 0, 8 * sizeof(uint64_t));
+    if (!d->d_stats) return 0;
+    HIP_OK(hipSetDevice(d->ordinal));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, d->d_stats, kStatCount * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (reset) HIP_OK(hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long)));
+    return 1;
 }

@@ -26,14 +26,17 @@ struct TraceArgs {
     uint32_t prev_count, frames, max_bounce;
     uint32_t n_groups, n_spheres, use_sky, flags;  // n_spheres: scalar rule set only
     uint32_t band_rows, band_count, band_index;
+    uint32_t sec_threshold;      // lanes that must wait for a secondary iteration
+    unsigned long long *stats;   // optional (RT_STATS): kStat* counters, NULL = off
 };
+enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatCount = 8 };
 
-// Dynamic LDS per block: rsqrt table + groups + materials.
+// Dynamic LDS per block: rsqrt table + fold table + groups + materials.
 static inline size_t rtk_lds_bytes(uint32_t n_groups) {
-    return 8192u + (size_t)n_groups * 64u + (size_t)n_groups * 128u;
+    return 8192u + 2048u + (size_t)n_groups * 64u + (size_t)n_groups * 128u;
 }
-static const uint32_t kMaxLdsGroups = (65536u - 8192u) / 192u;  // 298 groups = 1192 spheres
+static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / 192u;  // 288 groups = 1152 spheres
 
-extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, hipStream_t stream);
+extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

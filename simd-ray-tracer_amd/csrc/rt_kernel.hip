@@ -216,10 +216,16 @@ __device__ __forceinline__ Group load_group(const TraceArgs &a, const float4 *ld
         v2 = lds_groups[4 * g + 2];
         v3 = lds_groups[4 * g + 3];
     } else {
-        v0 = a.groups[4 * g + 0];
-        v1 = a.groups[4 * g + 1];
-        v2 = a.groups[4 * g + 2];
-        v3 = a.groups[4 * g + 3];
+        // constant address space: read-only for the kernel's lifetime, so a
+        // wave-uniform index always becomes an s_load into SGPRs
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(4))) v4f cv4f;
+        cv4f *cg = (cv4f *)a.groups;
+        const v4f w0 = cg[4 * g + 0], w1 = cg[4 * g + 1], w2 = cg[4 * g + 2], w3 = cg[4 * g + 3];
+        v0 = make_float4(w0.x, w0.y, w0.z, w0.w);
+        v1 = make_float4(w1.x, w1.y, w1.z, w1.w);
+        v2 = make_float4(w2.x, w2.y, w2.z, w2.w);
+        v3 = make_float4(w3.x, w3.y, w3.z, w3.w);
     }
     G.x[0] = v0.x; G.x[1] = v0.y; G.x[2] = v0.z; G.x[3] = v0.w;
     G.y[0] = v1.x; G.y[1] = v1.y; G.y[2] = v1.z; G.y[3] = v1.w;
@@ -236,27 +242,214 @@ __device__ __forceinline__ void sphere_core(const Sample &p, float sx, float sy,
     dist = dot3(qx, qy, qz, qx, qy, qz);
 }
 
-template <bool SIMD, int SRC>
-__global__ __launch_bounds__(256) void trace_kernel(TraceArgs a) {
+// Per-lane hit state.  SIMD rules: the reference's four lane minima
+// (MinT / MaterialIndex / InsideSphere, main.cpp:394-396), one per residue
+// class s & 3.  Scalar rules use slot 0 only (main.cpp:541-545).
+struct Hit {
+    float t0, t1, t2, t3;
+    uint32_t g0, g1, g2, g3;
+    uint32_t ins;
+};
+
+__device__ __forceinline__ void hit_reset(Hit &h) {
+    h.t0 = h.t1 = h.t2 = h.t3 = kFMax;
+    h.g0 = h.g1 = h.g2 = h.g3 = 0;
+    h.ins = 0;
+}
+
+struct Ray {  // passed by value so no callee ever loads the path state through a pointer
+    float ox, oy, oz, dx, dy, dz;
+};
+
+// Exact intersection of one candidate sphere (main.cpp:413-429 / 561-578),
+// given its T and |C - D*T|^2 from the packed distance test.
+template <bool SIMD, int L>
+__device__ __forceinline__ void candidate(Hit &h, uint32_t g, float T, float dist, float r2) {
+    const float X = __builtin_sqrtf(r2 - dist);
+    float it = T - X;
+    const bool in = it < kEps;
+    if (in) it = T + X;
+    if (SIMD) {
+        float &tl = L == 0 ? h.t0 : L == 1 ? h.t1 : L == 2 ? h.t2 : h.t3;
+        uint32_t &gl = L == 0 ? h.g0 : L == 1 ? h.g1 : L == 2 ? h.g2 : h.g3;
+        if (it < tl && it > kEps) {  // strict: the earliest group keeps a tie
+            tl = it;
+            gl = g;
+            h.ins |= (in ? 1u : 0u) << L;  // sticky OR (main.cpp:425)
+        }
+    } else {
+        if (!(it > h.t0) && !(it < kEps)) {  // the later sphere wins a tie
+            h.t0 = it;
+            h.g0 = 4u * g + (uint32_t)L;
+            h.ins = in ? 1u : 0u;
+        }
+    }
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// T and |C - D*T|^2 for two spheres of a group at once: every f32 op of
+// main.cpp:401-407 becomes one packed v_pk_{add,mul}_f32 over the pair (same
+// IEEE rounding per element; a packed op issues at the cost of a scalar one
+// on gfx950, so this halves the sphere loop's VALU instructions).
+__device__ __forceinline__ f2 pair_dist(const Ray r, f2 sx, f2 sy, f2 sz, f2 &T) {
+    const f2 ox = {r.ox, r.ox}, oy = {r.oy, r.oy}, oz = {r.oz, r.oz};
+    const f2 dx = {r.dx, r.dx}, dy = {r.dy, r.dy}, dz = {r.dz, r.dz};
+    const f2 cx = sx - ox, cy = sy - oy, cz = sz - oz;
+    T = (cx * dx + cy * dy) + cz * dz;
+    const f2 qx = cx - dx * T, qy = cy - dy * T, qz = cz - dz * T;
+    return (qx * qx + qy * qy) + qz * qz;
+}
+
+// All four spheres of group g; one wave-level branch per group, nested
+// branches only for the (rare) lanes that pass the distance test.
+template <bool SIMD>
+__device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const Ray p, Hit &h) {
+    f2 T01, T23;
+    const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
+    const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
+    bool h0, h1, h2, h3;
+    if (SIMD) {  // HitMask = d < r^2 (main.cpp:409)
+        h0 = d01.x < G.r2[0];
+        h1 = d01.y < G.r2[1];
+        h2 = d23.x < G.r2[2];
+        h3 = d23.y < G.r2[3];
+    } else {  // !(d > r^2) over the Count real spheres only (main.cpp:547,557)
+        const uint32_t s0 = 4u * g;
+        h0 = s0 + 0u < a.n_spheres && !(d01.x > G.r2[0]);
+        h1 = s0 + 1u < a.n_spheres && !(d01.y > G.r2[1]);
+        h2 = s0 + 2u < a.n_spheres && !(d23.x > G.r2[2]);
+        h3 = s0 + 3u < a.n_spheres && !(d23.y > G.r2[3]);
+    }
+    if (h0 | h1 | h2 | h3) {
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0]);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1]);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2]);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, G.r2[3]);
+    }
+}
+
+// Conservative per-wave culling for primary rays.  All primary rays of an
+// 8x8 tile start at CameraPosition and point into the tile's film rectangle
+// (+-0.5 px jitter), i.e. inside a cone (axis A, half-angle theta).  A
+// sphere can pass the exact test d < r^2 only if the LINE through the
+// camera along some cone direction comes within r of its centre, i.e. if the
+// angle between +-C and A is below theta + asin(r/|C|).  The test below uses
+// an angular margin of 2e-3 rad and r'^2 = r^2 + 1e-3|C|^2 + 1e-6, orders of
+// magnitude above the f32 rounding of the exact test, so a group it rejects
+// is one every lane's exact test would miss: skipping it changes nothing.
+struct Cone {
+    float ax, ay, az;     // axis
+    float cos_t, sin_t;   // inflated half-angle
+};
+
+__device__ __forceinline__ Cone tile_cone(const TraceArgs &a, float u0, float u1, float v0, float v1) {
+    const float fcx = a.film_center[0] - a.cam_pos[0];
+    const float fcy = a.film_center[1] - a.cam_pos[1];
+    const float fcz = a.film_center[2] - a.cam_pos[2];
+    const float aa[2] = {(-1.0f + (u0 * 2.0f) / (float)a.width) * a.film_w * 0.5f,
+                         (-1.0f + (u1 * 2.0f) / (float)a.width) * a.film_w * 0.5f};
+    const float bb[2] = {(-1.0f + (v0 * 2.0f) / (float)a.height) * a.film_h * 0.5f,
+                         (-1.0f + (v1 * 2.0f) / (float)a.height) * a.film_h * 0.5f};
+    float cx[4], cy[4], cz[4];
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+    for (int i = 0; i < 4; ++i) {
+        const float ka = aa[i & 1], kb = bb[i >> 1];
+        float x = fcx + ka * a.cam_x[0] + kb * a.cam_y[0];
+        float y = fcy + ka * a.cam_x[1] + kb * a.cam_y[1];
+        float z = fcz + ka * a.cam_x[2] + kb * a.cam_y[2];
+        const float inv = 1.0f / __builtin_sqrtf(x * x + y * y + z * z);
+        cx[i] = x * inv;
+        cy[i] = y * inv;
+        cz[i] = z * inv;
+        sx += cx[i];
+        sy += cy[i];
+        sz += cz[i];
+    }
+    Cone c;
+    const float inv = 1.0f / __builtin_sqrtf(sx * sx + sy * sy + sz * sz);
+    c.ax = sx * inv;
+    c.ay = sy * inv;
+    c.az = sz * inv;
+    float ct = 1.0f;
+    for (int i = 0; i < 4; ++i) ct = fminf(ct, c.ax * cx[i] + c.ay * cy[i] + c.az * cz[i]);
+    const float st = __builtin_sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
+    const float cd = 0.999998f, sd = 0.002f;  // cos/sin of the 2e-3 rad margin
+    c.cos_t = ct * cd - st * sd;
+    c.sin_t = st * cd + ct * sd;
+    return c;
+}
+
+__device__ __forceinline__ bool cone_may_hit(const TraceArgs &a, const Cone &c, float px, float py, float pz, float r2) {
+    if (!(r2 >= 0.0f)) return false;  // padding lanes of the scalar packing (-inf)
+    const float qx = px - a.cam_pos[0], qy = py - a.cam_pos[1], qz = pz - a.cam_pos[2];
+    const float c2 = qx * qx + qy * qy + qz * qz;
+    const float rr = r2 + 1e-3f * c2 + 1e-6f;
+    if (rr >= c2) return true;  // the camera is (nearly) inside: never cull
+    const float sb = __builtin_sqrtf(rr / c2), cb = __builtin_sqrtf(1.0f - rr / c2);
+    const float cos_lim = c.cos_t * cb - c.sin_t * sb;  // cos(theta + beta)
+    const float cos_phi = fabsf(c.ax * qx + c.ay * qy + c.az * qz) / __builtin_sqrtf(c2);
+    return cos_phi >= cos_lim - 1e-4f;
+}
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kMaxMaskWords = (kMaxLdsGroups + 63) / 64;
+constexpr uint32_t kFoldTable = 256;
+
+#ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) for the trace kernel
+#define RTK_MIN_WAVES_PER_SIMD 1
+#endif
+
+template <bool SIMD, int SRC, bool CULL>
+__global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(TraceArgs a) {
     extern __shared__ float4 smem[];
-    // LDS image: [rsqrt table 512 float4][groups 4*n_groups float4][materials 2*4*n_groups float4]
+    // LDS image: [rsqrt table 512 float4][fold table 128 float4]
+    //            [groups 4*n_groups float4][materials 8*n_groups float4]
+    __shared__ uint64_t s_mask[kWavesPerBlock][kMaxMaskWords];
     const float *lut = reinterpret_cast<const float *>(smem);
-    float4 *lds_groups = smem + 512;
+    float2 *fold = reinterpret_cast<float2 *>(smem + 512);
+    float4 *lds_groups = smem + 512 + kFoldTable / 2;
     float4 *lds_mats = lds_groups + 4 * a.n_groups;
     {
         const float4 *glut = reinterpret_cast<const float4 *>(a.rsqrt_lut);
         for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) smem[i] = glut[i];
         for (uint32_t i = threadIdx.x; i < 4u * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
         for (uint32_t i = threadIdx.x; i < 8u * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
-        __syncthreads();
+        // running-mean weights of frame k (main.cpp:484-487): 1/(p+1), p/(p+1)
+        for (uint32_t i = threadIdx.x; i < kFoldTable; i += blockDim.x) {
+            const uint32_t pc = a.prev_count + i;
+            fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
+        }
     }
 
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t ly = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const uint32_t x0 = blockIdx.x * 16u + (wave & 1u) * 8u;
+    const uint32_t ly0 = blockIdx.y * 16u + (wave >> 1) * 8u;
+    const uint32_t x = x0 + (lane & 7u);
+    const uint32_t ly = ly0 + (lane >> 3);
     const bool valid = x < a.width && ly < a.local_rows;
     const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
     const size_t pix = (size_t)ly * a.width + x;
+
+    const uint32_t n_words = (a.n_groups + 63u) / 64u;
+    if (CULL) {
+        // the wave's 8x8 tile; band_rows % 8 == 0 keeps its 8 rows contiguous
+        const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
+        const Cone c = tile_cone(a, (float)x0 - 0.501f, (float)x0 + 7.501f, (float)y0 - 0.501f, (float)y0 + 7.501f);
+        for (uint32_t w = 0; w < n_words; ++w) {
+            const uint32_t g = w * 64u + lane;
+            bool cand = false;
+            if (g < a.n_groups) {
+                const float4 gx = a.groups[4 * g + 0], gy = a.groups[4 * g + 1], gz = a.groups[4 * g + 2],
+                             gr = a.groups[4 * g + 3];
+                cand = cone_may_hit(a, c, gx.x, gy.x, gz.x, gr.x) || cone_may_hit(a, c, gx.y, gy.y, gz.y, gr.y) ||
+                       cone_may_hit(a, c, gx.z, gy.z, gz.z, gr.z) || cone_may_hit(a, c, gx.w, gy.w, gz.w, gr.w);
+            }
+            const uint64_t m = __ballot(cand);
+            if (lane == 0) s_mask[wave][w] = m;
+        }
+    }
+    __syncthreads();
 
     float accx = 0.0f, accy = 0.0f, accz = 0.0f;
     if (valid && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
@@ -266,59 +459,62 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs a) {
         accz = pv.z;
     }
 
-    uint32_t nrays = 0;
-    uint32_t k = 0;
-    bool active = valid && a.frames > 0;
+    // lane mode: 0 = next primary ray pending, 1 = path continues (secondary), 2 = done
+    uint32_t mode = (valid && a.frames > 0) ? 0u : 2u;
+    uint32_t k = 0, nrays = 0;
+    uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0;  // wave-uniform
     Sample p;
-    if (active) start_sample(a, x, y, a.prev_count, p);
+    p.bounce = 0;
+    if (a.max_bounce == 0 && mode == 0u) {  // no segment is traced; every frame folds black
+        for (; k < a.frames; ++k) {
+            const uint32_t pc = a.prev_count + k;
+            const float inv = k < kFoldTable ? fold[k].x : 1.0f / (float)(pc + 1u);
+            const float ratio = k < kFoldTable ? fold[k].y : (float)pc / (float)(pc + 1u);
+            accx = 0.0f * inv + accx * ratio;
+            accy = 0.0f * inv + accy * ratio;
+            accz = 0.0f * inv + accz * ratio;
+        }
+        mode = 2u;
+    }
 
-    while (active) {
-        bool done;
-        if (a.max_bounce == 0) {
-            done = true;
-        } else {
+    for (;;) {
+        const uint64_t pri = __ballot(mode == 0u);
+        const uint64_t sec = __ballot(mode == 1u);
+        if ((pri | sec) == 0) break;
+        // Secondary segments run the full sphere loop; let them gather until
+        // enough lanes share one (or no primary work is left).
+        // (every iteration advances at least one lane: no empty iteration type)
+        const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        if (a.stats) {
+            if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
+            else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
+        }
+        if (do_sec ? mode == 1u : mode == 0u) {
+            if (!do_sec) start_sample(a, x, y, a.prev_count + k, p);
             nrays += 1;
-            // ---- brute-force intersection against every sphere (main.cpp:392-441 / 541-588)
-            float t0 = kFMax, t1 = kFMax, t2 = kFMax, t3 = kFMax;
-            uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, ins = 0;
-            for (uint32_t g = 0; g < a.n_groups; ++g) {
-                const Group G = load_group<SRC>(a, lds_groups, g);
-#pragma unroll
-                for (int l = 0; l < 4; ++l) {
-                    float T, dist;
-                    sphere_core(p, G.x[l], G.y[l], G.z[l], T, dist);
-                    const float r2 = G.r2[l];
-                    if (SIMD) {
-                        // lane-4 rules: strict '<' hit, per-class strict minimum,
-                        // sticky inside flag (main.cpp:409-429)
-                        if (dist < r2) {
-                            const float X = __builtin_sqrtf(r2 - dist);
-                            float it = T - X;
-                            const bool in = it < kEps;
-                            if (in) it = T + X;
-                            float &tl = l == 0 ? t0 : l == 1 ? t1 : l == 2 ? t2 : t3;
-                            uint32_t &gl = l == 0 ? g0 : l == 1 ? g1 : l == 2 ? g2 : g3;
-                            if (it < tl && it > kEps) {
-                                tl = it;
-                                gl = g;
-                                ins |= (in ? 1u : 0u) << l;
-                            }
-                        }
-                    } else {
-                        // scalar rules: '<=' hit, later sphere wins ties, inside
-                        // flag from the accepted sphere only (main.cpp:557-578)
-                        if (4u * g + (uint32_t)l < a.n_spheres && !(dist > r2)) {
-                            const float X = __builtin_sqrtf(r2 - dist);
-                            float it = T - X;
-                            const bool in = it < kEps;
-                            if (in) it = T + X;
-                            if (!(it > t0) && !(it < kEps)) {
-                                t0 = it;
-                                g0 = 4u * g + (uint32_t)l;
-                                ins = in ? 1u : 0u;
-                            }
-                        }
+            Hit h;
+            hit_reset(h);
+            const Ray ray = {p.ox, p.oy, p.oz, p.dx, p.dy, p.dz};
+            if (CULL && !do_sec) {
+                for (uint32_t w = 0; w < n_words; ++w) {
+                    uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
+                                 ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32)) << 32);
+                    if (a.stats) st_groups += __builtin_popcountll(m);
+                    while (m) {
+                        const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
+                        m &= m - 1;
+                        test_group<SIMD>(a, load_group<SRC>(a, lds_groups, g), g, ray, h);
                     }
+                }
+            } else {
+                // software-pipelined: group g+1's scalar load is in flight
+                // while group g is tested (the group array carries one
+                // padding group, so g+1 is always a valid address)
+                Group next = load_group<SRC>(a, lds_groups, 0);
+                for (uint32_t g = 0; g < a.n_groups; ++g) {
+                    const Group G = next;
+                    next = load_group<SRC>(a, lds_groups, g + 1u);
+                    test_group<SIMD>(a, G, g, ray, h);
                 }
             }
             // ---- hit select (x64_math.h:579-585 HorizontalMin + first equal lane)
@@ -326,18 +522,19 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs a) {
             uint32_t sidx;
             bool inside;
             if (SIMD) {
-                const float m02 = t0 < t2 ? t0 : t2;
-                const float m13 = t1 < t3 ? t1 : t3;
+                const float m02 = h.t0 < h.t2 ? h.t0 : h.t2;
+                const float m13 = h.t1 < h.t3 ? h.t1 : h.t3;
                 tmin = m02 < m13 ? m02 : m13;
-                const uint32_t l = t0 == tmin ? 0u : t1 == tmin ? 1u : t2 == tmin ? 2u : 3u;
-                const uint32_t gsel = l == 0 ? g0 : l == 1 ? g1 : l == 2 ? g2 : g3;
+                const uint32_t l = h.t0 == tmin ? 0u : h.t1 == tmin ? 1u : h.t2 == tmin ? 2u : 3u;
+                const uint32_t gsel = l == 0 ? h.g0 : l == 1 ? h.g1 : l == 2 ? h.g2 : h.g3;
                 sidx = gsel * 4u + l;
-                inside = (ins >> l) & 1u;
+                inside = (h.ins >> l) & 1u;
             } else {
-                tmin = t0;
-                sidx = g0;
-                inside = ins != 0;
+                tmin = h.t0;
+                sidx = h.g0;
+                inside = h.ins != 0;
             }
+            bool done;
             if (tmin == kFMax) {
                 if (a.use_sky) {  // main.cpp:434-438
                     const float s = (p.dy + 1.0f) * 0.5f;
@@ -364,22 +561,19 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs a) {
                 p.bounce += 1;
                 done = p.bounce == a.max_bounce;
             }
-        }
-        if (done) {
-            // ---- running-mean blend (main.cpp:484-489)
-            const uint32_t pc = a.prev_count + k;
-            const uint32_t total = pc + 1u;
-            const float inv = 1.0f / (float)total;
-            const float ratio = (float)pc / (float)total;
-            const float ox = a.max_bounce == 0 ? 0.0f : p.cx;
-            const float oy = a.max_bounce == 0 ? 0.0f : p.cy;
-            const float oz = a.max_bounce == 0 ? 0.0f : p.cz;
-            accx = ox * inv + accx * ratio;
-            accy = oy * inv + accy * ratio;
-            accz = oz * inv + accz * ratio;
-            k += 1;
-            if (k < a.frames) start_sample(a, x, y, a.prev_count + k, p);
-            else active = false;
+            if (done) {
+                // ---- running-mean blend (main.cpp:484-489)
+                const uint32_t pc = a.prev_count + k;
+                const float inv = k < kFoldTable ? fold[k].x : 1.0f / (float)(pc + 1u);
+                const float ratio = k < kFoldTable ? fold[k].y : (float)pc / (float)(pc + 1u);
+                accx = p.cx * inv + accx * ratio;
+                accy = p.cy * inv + accy * ratio;
+                accz = p.cz * inv + accz * ratio;
+                k += 1;
+                mode = k < a.frames ? 0u : 2u;
+            } else {
+                mode = 1u;
+            }
         }
     }
 
@@ -394,6 +588,13 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceArgs a) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
     if (lane == 0 && sum) atomicAdd(a.rays, (unsigned long long)sum);
+    if (a.stats && lane == 0) {
+        atomicAdd(a.stats + kStatPriIters, (unsigned long long)st_pri_it);
+        atomicAdd(a.stats + kStatPriLanes, (unsigned long long)st_pri_lanes);
+        atomicAdd(a.stats + kStatSecIters, (unsigned long long)st_sec_it);
+        atomicAdd(a.stats + kStatSecLanes, (unsigned long long)st_sec_lanes);
+        atomicAdd(a.stats + kStatPriGroups, (unsigned long long)st_groups);
+    }
 }
 
 // Scatter RCCL-gathered compact band images into the full framebuffer.
@@ -420,17 +621,23 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint8_t *src, uint6
 
 }  // namespace rtk
 
-extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, hipStream_t stream) {
+extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream) {
     const dim3 block(256);
     const dim3 grid((a->width + 15u) / 16u, (a->local_rows + 15u) / 16u);
     const size_t lds = rtk_lds_bytes(a->n_groups);
-    if (simd) {
-        if (src == kSrcLds) hipLaunchKernelGGL((rtk::trace_kernel<true, kSrcLds>), grid, block, lds, stream, *a);
-        else hipLaunchKernelGGL((rtk::trace_kernel<true, kSrcSmem>), grid, block, lds, stream, *a);
-    } else {
-        if (src == kSrcLds) hipLaunchKernelGGL((rtk::trace_kernel<false, kSrcLds>), grid, block, lds, stream, *a);
-        else hipLaunchKernelGGL((rtk::trace_kernel<false, kSrcSmem>), grid, block, lds, stream, *a);
+#define RTK_LAUNCH(S, R, C) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C>), grid, block, lds, stream, *a)
+    const int key = (simd ? 4 : 0) | (src == kSrcLds ? 2 : 0) | (cull ? 1 : 0);
+    switch (key) {
+        case 0: RTK_LAUNCH(false, kSrcSmem, false); break;
+        case 1: RTK_LAUNCH(false, kSrcSmem, true); break;
+        case 2: RTK_LAUNCH(false, kSrcLds, false); break;
+        case 3: RTK_LAUNCH(false, kSrcLds, true); break;
+        case 4: RTK_LAUNCH(true, kSrcSmem, false); break;
+        case 5: RTK_LAUNCH(true, kSrcSmem, true); break;
+        case 6: RTK_LAUNCH(true, kSrcLds, false); break;
+        default: RTK_LAUNCH(true, kSrcLds, true); break;
     }
+#undef RTK_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
