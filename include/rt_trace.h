@@ -215,9 +215,15 @@ int rt_device_synchronize(rt_device *dev);
 /* Scheduling counters accumulated over trace launches when the process runs
  * with RT_STATS=1: [0] primary wave-iterations, [1] primary lane-segments,
  * [2] secondary wave-iterations, [3] secondary lane-segments, [4] sphere
- * groups tested by primary iterations after culling.  Returns 1 when
- * enabled, 0 when not (out zeroed), negative on error. */
-int rt_debug_stats(rt_device *dev, uint64_t out[8], int reset);
+ * groups tested by primary iterations after culling, [5] secondary groups
+ * where some lane passed the distance test, [8..13] diagnostic-build cycle
+ * stamps.  Returns 1 when enabled, 0 when not (out zeroed), < 0 on error. */
+int rt_debug_stats(rt_device *dev, uint64_t out[16], int reset);
+
+/* With RT_WAVETIMES=1: {start, end} s_memrealtime (100 MHz) of every wave of
+ * the last trace launch, wave id = (blockIdx.y*gridDim.x + blockIdx.x)*4 + w.
+ * Returns the number of waves copied (0 when disabled), < 0 on error. */
+int64_t rt_debug_wave_times(rt_device *dev, uint64_t *out, uint64_t max_waves);
 const char *rt_last_error(void);
 
 /* ----------------------------------------------- OnInit / OnRender driver */

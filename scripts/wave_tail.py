@@ -1,0 +1,37 @@
+"""Diagnostic: per-wave start/end times of one C2 launch -> occupancy over time."""
+import os
+import sys
+import pathlib
+import numpy as np
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+os.environ["RT_WAVETIMES"] = "1"
+import torch
+import __graft_entry__ as graft
+rt = graft.load_package()
+W, H, S, B, N = 1920, 1080, int(os.environ.get("SPP", "256")), 8, 64
+scene = rt.scene_prefix(rt.scene_builtin(1), N)
+cam = rt.camera_setup(scene, W, H)
+dev = rt.Device(0)
+dev.upload_scene(scene)
+prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+for _ in range(2):
+    dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
+              frames=S, max_bounce=B, accum_zero=True)
+torch.cuda.synchronize()
+wt = dev.debug_wave_times().astype(np.int64)
+t0 = wt[:, 0].min()
+st, en = (wt[:, 0] - t0) / 100.0, (wt[:, 1] - t0) / 100.0  # microseconds
+dur = en - st
+print(f"waves {len(wt)}  kernel span {en.max():.0f} us  wave dur mean {dur.mean():.0f} p50 {np.median(dur):.0f} "
+      f"p90 {np.percentile(dur, 90):.0f} max {dur.max():.0f} us")
+T = en.max()
+for f in np.linspace(0, 1, 21)[:-1]:
+    t = f * T
+    print(f"t={t:8.0f}us active waves {int(((st <= t) & (en > t)).sum()):6d}")
+gx = (W + 15) // 16
+wid = np.arange(len(wt))
+bx, by, w = (wid // 4) % gx, (wid // 4) // gx, wid % 4
+slow = np.argsort(-dur)[:10]
+print("slowest waves (tile x,y):", [(int(bx[i] * 16 + (w[i] & 1) * 8), int(by[i] * 16 + (w[i] >> 1) * 8), int(dur[i])) for i in slow])

@@ -109,6 +109,7 @@ SIGNATURES = {
                                   c_void_p]),
     "rt_device_synchronize": (c_int, [c_void_p]),
     "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
+    "rt_debug_wave_times": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
     "rt_last_error": (c_char_p, []),
     "rt_on_init": (c_int, [POINTER(RtInitParams)]),
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
@@ -259,13 +260,21 @@ class Device:
 
     def debug_stats(self, reset: bool = True):
         """RT_STATS=1 scheduling counters (see rt_debug_stats), or None when disabled."""
-        out = np.zeros(8, np.uint64)
+        out = np.zeros(16, np.uint64)
         rc = lib().rt_debug_stats(self.handle, out.ctypes.data, int(reset))
         _check(rc, "rt_debug_stats")
         if rc == 0:
             return None
-        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups"]
-        return {k: int(v) for k, v in zip(keys, out)}
+        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups", "_6", "_7",
+                "cyc_pri_isect", "cyc_pri_shade", "cyc_pri_fold", "cyc_sec_isect", "cyc_sec_shade", "cyc_sec_fold"]
+        return {k: int(v) for k, v in zip(keys, out) if not k.startswith("_")}
+
+    def debug_wave_times(self, max_waves: int = 1 << 22):
+        """RT_WAVETIMES=1: (n, 2) array of per-wave {start, end} (100 MHz ticks), or None."""
+        out = np.zeros(2 * max_waves, np.uint64)
+        n = int(lib().rt_debug_wave_times(self.handle, out.ctypes.data, max_waves))
+        _check(n, "rt_debug_wave_times")
+        return out[: 2 * n].reshape(-1, 2) if n else None
 
     def synchronize(self) -> None:
         _check(lib().rt_device_synchronize(self.handle), "rt_device_synchronize")

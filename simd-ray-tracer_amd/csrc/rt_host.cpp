@@ -27,7 +27,11 @@ struct rt_device {
     int src = kSrcSmem;
     int cull = 1;
     uint32_t sec_threshold = 16;
+    int lanes_per_pixel = 4;
     unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
+    unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
+    size_t wave_times_cap = 0;
+    bool want_wave_times = false;
 };
 
 static thread_local char g_err[512];
@@ -68,6 +72,10 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (cull && cull[0] == '0') d->cull = 0;
     const char *thr = getenv("RT_SEC_THRESHOLD");
     if (thr) d->sec_threshold = (uint32_t)atoi(thr);
+    const char *wt = getenv("RT_WAVETIMES");
+    d->want_wave_times = wt && wt[0] == '1';
+    const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
+    if (lp) d->lanes_per_pixel = atoi(lp) == 1 ? 1 : atoi(lp) == 2 ? 2 : 4;
     const char *st = getenv("RT_STATS");
     if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatCount * sizeof(unsigned long long)) == hipSuccess)
         (void)hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long));
@@ -85,6 +93,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
     }
     (void)hipFree(d->d_lut);
     (void)hipFree(d->d_stats);
+    (void)hipFree(d->d_wave_times);
     (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
@@ -234,9 +243,19 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.band_index = desc->BandIndex;
     a.sec_threshold = d->sec_threshold;
     a.stats = d->d_stats;
+    if (d->want_wave_times) {
+        const size_t waves = (size_t)((desc->Width + 7u) / 8u) * ((local_rows + 7u) / 8u) * 4u * 4u;  // >= any shape
+        if (waves > d->wave_times_cap) {
+            (void)hipFree(d->d_wave_times);
+            d->d_wave_times = nullptr;
+            if (hipMalloc(&d->d_wave_times, waves * 16u) != hipSuccess) return fail(RT_ENOMEM, "wave_times");
+            d->wave_times_cap = waves;
+        }
+        a.wave_times = d->d_wave_times;
+    }
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, s) != 0)
+    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, d->lanes_per_pixel, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return RT_OK;
 }
@@ -262,13 +281,23 @@ extern "C" int rt_device_synchronize(rt_device *d) {
     return RT_OK;
 }
 
-extern "C" int rt_debug_stats(rt_device *d, uint64_t out[8], int reset) {
+extern "C" int rt_debug_stats(rt_device *d, uint64_t out[16], int reset) {
     if (!d || !out) return fail(RT_EINVAL, "rt_debug_stats: NULL argument");
-    memset(out, 0, 8 * sizeof(uint64_t));
+    memset(out, 0, 16 * sizeof(uint64_t));
     if (!d->d_stats) return 0;
     HIP_OK(hipSetDevice(d->ordinal));
     HIP_OK(hipDeviceSynchronize());
     HIP_OK(hipMemcpy(out, d->d_stats, kStatCount * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (reset) HIP_OK(hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long)));
     return 1;
+}
+
+extern "C" int64_t rt_debug_wave_times(rt_device *d, uint64_t *out, uint64_t max_waves) {
+    if (!d || !out) return fail(RT_EINVAL, "rt_debug_wave_times: NULL argument");
+    if (!d->d_wave_times) return 0;
+    const uint64_t n = max_waves < d->wave_times_cap ? max_waves : d->wave_times_cap;
+    HIP_OK(hipSetDevice(d->ordinal));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, d->d_wave_times, n * 16u, hipMemcpyDeviceToHost));
+    return (int64_t)n;
 }

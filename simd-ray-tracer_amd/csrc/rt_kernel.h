@@ -28,8 +28,11 @@ struct TraceArgs {
     uint32_t band_rows, band_count, band_index;
     uint32_t sec_threshold;      // lanes that must wait for a secondary iteration
     unsigned long long *stats;   // optional (RT_STATS): kStat* counters, NULL = off
+    unsigned long long *wave_times;  // optional (RT_WAVETIMES): per-wave {start, end} s_memrealtime
 };
-enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatCount = 8 };
+enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
+       kStatStamp = 8,  // RTK_DIAG_STAMPS: cycles in {pri,sec} x {intersect, select+shade, fold}
+       kStatCount = 16 };
 
 // Dynamic LDS per block: rsqrt table + fold table + groups + materials.
 static inline size_t rtk_lds_bytes(uint32_t n_groups) {
@@ -37,6 +40,7 @@ static inline size_t rtk_lds_bytes(uint32_t n_groups) {
 }
 static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / 192u;  // 288 groups = 1152 spheres
 
-extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream);
+extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
+                                hipStream_t stream);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

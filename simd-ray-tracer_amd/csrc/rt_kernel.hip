@@ -265,7 +265,11 @@ struct Ray {  // passed by value so no callee ever loads the path state through 
 // given its T and |C - D*T|^2 from the packed distance test.
 template <bool SIMD, int L>
 __device__ __forceinline__ void candidate(Hit &h, uint32_t g, float T, float dist, float r2) {
+#ifdef RTK_DIAG_FAST_SQRT  // timing diagnostic only: 1-ulp hardware sqrt, not bit-exact
+    const float X = __builtin_amdgcn_sqrtf(r2 - dist);
+#else
     const float X = __builtin_sqrtf(r2 - dist);
+#endif
     float it = T - X;
     const bool in = it < kEps;
     if (in) it = T + X;
@@ -304,7 +308,8 @@ __device__ __forceinline__ f2 pair_dist(const Ray r, f2 sx, f2 sy, f2 sz, f2 &T)
 // All four spheres of group g; one wave-level branch per group, nested
 // branches only for the (rare) lanes that pass the distance test.
 template <bool SIMD>
-__device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const Ray p, Hit &h) {
+__device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const Ray p, Hit &h,
+                                           uint32_t *hit_groups = nullptr) {
     f2 T01, T23;
     const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
     const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
@@ -321,7 +326,13 @@ __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, u
         h2 = s0 + 2u < a.n_spheres && !(d23.x > G.r2[2]);
         h3 = s0 + 3u < a.n_spheres && !(d23.y > G.r2[3]);
     }
+    if (hit_groups && __ballot(h0 | h1 | h2 | h3)) *hit_groups += 1;
+#ifdef RTK_DIAG_NO_CANDIDATE  // timing diagnostic only: wrong results
+    h.ins |= (h0 | h1 | h2 | h3) ? 16u : 0u;
+    if (false) {
+#else
     if (h0 | h1 | h2 | h3) {
+#endif
         if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0]);
         if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1]);
         if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2]);
@@ -395,17 +406,35 @@ __device__ __forceinline__ bool cone_may_hit(const TraceArgs &a, const Cone &c, 
 constexpr int kWavesPerBlock = 4;
 constexpr int kMaxMaskWords = (kMaxLdsGroups + 63) / 64;
 constexpr uint32_t kFoldTable = 256;
+constexpr uint32_t kRing = 8;  // per-pixel out-of-order sample slots (LDS)
 
 #ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) for the trace kernel
 #define RTK_MIN_WAVES_PER_SIMD 1
 #endif
 
-template <bool SIMD, int SRC, bool CULL>
+// Work shape.  A wave owns a small pixel tile and P lanes per pixel: lane
+// j of a pixel traces that pixel's samples k = j, j+P, j+2P, ... (any order
+// across lanes), parks each finished sample's radiance in a per-pixel LDS
+// ring, and the pixel's owner lane (j == 0) folds the ring into the running
+// mean strictly in sample order (main.cpp:484-487), so results are
+// bit-identical to one lane tracing the samples one after another.  P > 1
+// splits the long per-pixel sample chains of pixels that see geometry over
+// several lanes: the heaviest waves get P times shorter, which removes most
+// of the kernel's tail.  Tiles: P=1 8x8, P=2 8x4, P=4 4x4 pixels per wave.
+template <int P>
+struct Shape {
+    static constexpr uint32_t TW = P == 4 ? 4u : 8u;
+    static constexpr uint32_t TH = P == 1 ? 8u : 4u;
+};
+
+template <bool SIMD, int SRC, bool CULL, int P>
 __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(TraceArgs a) {
+    constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
     extern __shared__ float4 smem[];
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
     __shared__ uint64_t s_mask[kWavesPerBlock][kMaxMaskWords];
+    __shared__ float4 s_ring[P > 1 ? kWavesPerBlock * NPIX * kRing : 1];
     const float *lut = reinterpret_cast<const float *>(smem);
     float2 *fold = reinterpret_cast<float2 *>(smem + 512);
     float4 *lds_groups = smem + 512 + kFoldTable / 2;
@@ -420,22 +449,29 @@ __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(Trac
             const uint32_t pc = a.prev_count + i;
             fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
         }
+        if (P > 1)
+            for (uint32_t i = threadIdx.x; i < kWavesPerBlock * NPIX * kRing; i += blockDim.x)
+                s_ring[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    const uint32_t x0 = blockIdx.x * 16u + (wave & 1u) * 8u;
-    const uint32_t ly0 = blockIdx.y * 16u + (wave >> 1) * 8u;
-    const uint32_t x = x0 + (lane & 7u);
-    const uint32_t ly = ly0 + (lane >> 3);
+    const uint64_t t_start = a.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint32_t x0 = blockIdx.x * (2u * TW) + (wave & 1u) * TW;
+    const uint32_t ly0 = blockIdx.y * (2u * TH) + (wave >> 1) * TH;
+    const uint32_t pl = lane / P, j = lane % P;  // pixel of the tile, sample lane of the pixel
+    const uint32_t x = x0 + pl % TW;
+    const uint32_t ly = ly0 + pl / TW;
     const bool valid = x < a.width && ly < a.local_rows;
     const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
-    const size_t pix = (size_t)ly * a.width + x;
+    const bool owner = j == 0;
+    float4 *ring = s_ring + (wave * NPIX + pl) * kRing;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     if (CULL) {
-        // the wave's 8x8 tile; band_rows % 8 == 0 keeps its 8 rows contiguous
+        // the wave's tile; band_rows % 8 == 0 keeps its TH rows contiguous
         const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
-        const Cone c = tile_cone(a, (float)x0 - 0.501f, (float)x0 + 7.501f, (float)y0 - 0.501f, (float)y0 + 7.501f);
+        const Cone c = tile_cone(a, (float)x0 - 0.501f, (float)(x0 + TW - 1u) + 0.501f, (float)y0 - 0.501f,
+                                 (float)(y0 + TH - 1u) + 0.501f);
         for (uint32_t w = 0; w < n_words; ++w) {
             const uint32_t g = w * 64u + lane;
             bool cand = false;
@@ -452,132 +488,160 @@ __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(Trac
     __syncthreads();
 
     float accx = 0.0f, accy = 0.0f, accz = 0.0f;
-    if (valid && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
-        const float4 pv = a.prev[pix];
+    if (valid && owner && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
+        const float4 pv = a.prev[(size_t)ly * a.width + x];
         accx = pv.x;
         accy = pv.y;
         accz = pv.z;
     }
 
-    // lane mode: 0 = next primary ray pending, 1 = path continues (secondary), 2 = done
-    uint32_t mode = (valid && a.frames > 0) ? 0u : 2u;
-    uint32_t k = 0, nrays = 0;
-    uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0;  // wave-uniform
+    // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left
+    uint32_t k = j;            // this lane's next (or current) sample
+    uint32_t folded = 0;       // owner: samples folded so far
+    uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
+    uint32_t nrays = 0;
+    uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
     Sample p;
     p.bounce = 0;
-    if (a.max_bounce == 0 && mode == 0u) {  // no segment is traced; every frame folds black
-        for (; k < a.frames; ++k) {
-            const uint32_t pc = a.prev_count + k;
-            const float inv = k < kFoldTable ? fold[k].x : 1.0f / (float)(pc + 1u);
-            const float ratio = k < kFoldTable ? fold[k].y : (float)pc / (float)(pc + 1u);
-            accx = 0.0f * inv + accx * ratio;
-            accy = 0.0f * inv + accy * ratio;
-            accz = 0.0f * inv + accz * ratio;
-        }
-        mode = 2u;
-    }
+    p.cx = p.cy = p.cz = 0.0f;
 
     for (;;) {
-        const uint64_t pri = __ballot(mode == 0u);
+        // ring space: sample k may start once k < folded + kRing (the oldest
+        // unfolded sample's lane is never blocked, so this cannot deadlock)
+        const uint32_t folded_g = P > 1 ? (uint32_t)__shfl(folded, (int)(lane - j), 64) : folded;
+        const bool can_start = mode == 0u && (P == 1 || k < folded_g + kRing);
+        const uint64_t pri = __ballot(can_start);
         const uint64_t sec = __ballot(mode == 1u);
-        if ((pri | sec) == 0) break;
-        // Secondary segments run the full sphere loop; let them gather until
-        // enough lanes share one (or no primary work is left).
-        // (every iteration advances at least one lane: no empty iteration type)
-        const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
-        if (a.stats) {
-            if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
-            else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
-        }
-        if (do_sec ? mode == 1u : mode == 0u) {
-            if (!do_sec) start_sample(a, x, y, a.prev_count + k, p);
-            nrays += 1;
-            Hit h;
-            hit_reset(h);
-            const Ray ray = {p.ox, p.oy, p.oz, p.dx, p.dy, p.dz};
-            if (CULL && !do_sec) {
-                for (uint32_t w = 0; w < n_words; ++w) {
-                    uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
-                                 ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32)) << 32);
-                    if (a.stats) st_groups += __builtin_popcountll(m);
-                    while (m) {
-                        const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
-                        m &= m - 1;
-                        test_group<SIMD>(a, load_group<SRC>(a, lds_groups, g), g, ray, h);
+        const uint64_t alive = __ballot(mode != 2u || (owner && valid && folded < a.frames));
+        if (alive == 0) break;
+        if ((pri | sec) != 0) {
+            // Secondary segments run the full sphere loop; let them gather until
+            // enough lanes share one (or no primary work is ready).
+            const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+            if (a.stats) {
+                if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
+                else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
+            }
+            if (do_sec ? mode == 1u : can_start) {
+                if (!do_sec) start_sample(a, x, y, a.prev_count + k, p);
+                bool done;
+                if (a.max_bounce == 0) {
+                    done = true;  // no segment is traced; the frame folds black
+                } else {
+                    nrays += 1;
+                    Hit h;
+                    hit_reset(h);
+                    const Ray ray = {p.ox, p.oy, p.oz, p.dx, p.dy, p.dz};
+                    if (CULL && !do_sec) {
+                        for (uint32_t w = 0; w < n_words; ++w) {
+                            uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
+                                         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32))
+                                          << 32);
+                            if (a.stats) st_groups += __builtin_popcountll(m);
+                            while (m) {
+                                const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
+                                m &= m - 1;
+                                test_group<SIMD>(a, load_group<SRC>(a, lds_groups, g), g, ray, h);
+                            }
+                        }
+                    } else {
+                        // software-pipelined: group g+1's scalar load is in flight
+                        // while group g is tested (the group array carries one
+                        // padding group, so g+1 is always a valid address)
+                        Group next = load_group<SRC>(a, lds_groups, 0);
+                        for (uint32_t g = 0; g < a.n_groups; ++g) {
+                            const Group G = next;
+                            next = load_group<SRC>(a, lds_groups, g + 1u);
+                            test_group<SIMD>(a, G, g, ray, h, a.stats ? &st_sec_hit : nullptr);
+                        }
+                    }
+                    // ---- hit select (x64_math.h:579-585 HorizontalMin + first equal lane)
+                    float tmin;
+                    uint32_t sidx;
+                    bool inside;
+                    if (SIMD) {
+                        const float m02 = h.t0 < h.t2 ? h.t0 : h.t2;
+                        const float m13 = h.t1 < h.t3 ? h.t1 : h.t3;
+                        tmin = m02 < m13 ? m02 : m13;
+                        const uint32_t l = h.t0 == tmin ? 0u : h.t1 == tmin ? 1u : h.t2 == tmin ? 2u : 3u;
+                        const uint32_t gsel = l == 0 ? h.g0 : l == 1 ? h.g1 : l == 2 ? h.g2 : h.g3;
+                        sidx = gsel * 4u + l;
+                        inside = (h.ins >> l) & 1u;
+                    } else {
+                        tmin = h.t0;
+                        sidx = h.g0;
+                        inside = h.ins != 0;
+                    }
+                    if (tmin == kFMax) {
+                        if (a.use_sky) {  // main.cpp:434-438
+                            const float s = (p.dy + 1.0f) * 0.5f;
+                            const float w = (1.0f - s) * 1.0f;
+                            p.cx = p.cx + (w + s * 0.5f) * p.ax;
+                            p.cy = p.cy + (w + s * 0.7f) * p.ay;
+                            p.cz = p.cz + (w + s * 1.0f) * p.az;
+                        }
+                        done = true;
+                    } else {
+                        // Re-derive the winner's HitNormal / NextRayOrigin exactly as
+                        // they were formed at acceptance (main.cpp:423-429).
+                        const float *gsph = reinterpret_cast<const float *>(lds_groups) + 16u * (sidx >> 2) + (sidx & 3u);
+                        const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
+                        const float cx = sx - p.ox, cy = sy - p.oy, cz = sz - p.oz;
+                        const float ipx = p.dx * tmin, ipy = p.dy * tmin, ipz = p.dz * tmin;
+                        const float hx = ipx - cx, hy = ipy - cy, hz = ipz - cz;
+                        p.ox = p.ox + ipx;
+                        p.oy = p.oy + ipy;
+                        p.oz = p.oz + ipz;
+                        const float4 cs = lds_mats[2u * sidx + 0u];
+                        const float4 ei = lds_mats[2u * sidx + 1u];
+                        shade(lut, cs, ei, hx, hy, hz, inside, p);
+                        p.bounce += 1;
+                        done = p.bounce == a.max_bounce;
                     }
                 }
-            } else {
-                // software-pipelined: group g+1's scalar load is in flight
-                // while group g is tested (the group array carries one
-                // padding group, so g+1 is always a valid address)
-                Group next = load_group<SRC>(a, lds_groups, 0);
-                for (uint32_t g = 0; g < a.n_groups; ++g) {
-                    const Group G = next;
-                    next = load_group<SRC>(a, lds_groups, g + 1u);
-                    test_group<SIMD>(a, G, g, ray, h);
+                if (done) {
+                    const float ox = a.max_bounce == 0 ? 0.0f : p.cx;
+                    const float oy = a.max_bounce == 0 ? 0.0f : p.cy;
+                    const float oz = a.max_bounce == 0 ? 0.0f : p.cz;
+                    if (P == 1) {
+                        // ---- running-mean blend (main.cpp:484-489), in order by construction
+                        const uint32_t pc = a.prev_count + k;
+                        const float inv = k < kFoldTable ? fold[k].x : 1.0f / (float)(pc + 1u);
+                        const float ratio = k < kFoldTable ? fold[k].y : (float)pc / (float)(pc + 1u);
+                        accx = ox * inv + accx * ratio;
+                        accy = oy * inv + accy * ratio;
+                        accz = oz * inv + accz * ratio;
+                        folded = k + 1u;
+                    } else {
+                        ring[k % kRing] = make_float4(ox, oy, oz, 1.0f);  // ready
+                    }
+                    k += P;
+                    mode = k < a.frames ? 0u : 2u;
+                } else {
+                    mode = 1u;
                 }
             }
-            // ---- hit select (x64_math.h:579-585 HorizontalMin + first equal lane)
-            float tmin;
-            uint32_t sidx;
-            bool inside;
-            if (SIMD) {
-                const float m02 = h.t0 < h.t2 ? h.t0 : h.t2;
-                const float m13 = h.t1 < h.t3 ? h.t1 : h.t3;
-                tmin = m02 < m13 ? m02 : m13;
-                const uint32_t l = h.t0 == tmin ? 0u : h.t1 == tmin ? 1u : h.t2 == tmin ? 2u : 3u;
-                const uint32_t gsel = l == 0 ? h.g0 : l == 1 ? h.g1 : l == 2 ? h.g2 : h.g3;
-                sidx = gsel * 4u + l;
-                inside = (h.ins >> l) & 1u;
-            } else {
-                tmin = h.t0;
-                sidx = h.g0;
-                inside = h.ins != 0;
-            }
-            bool done;
-            if (tmin == kFMax) {
-                if (a.use_sky) {  // main.cpp:434-438
-                    const float s = (p.dy + 1.0f) * 0.5f;
-                    const float w = (1.0f - s) * 1.0f;
-                    p.cx = p.cx + (w + s * 0.5f) * p.ax;
-                    p.cy = p.cy + (w + s * 0.7f) * p.ay;
-                    p.cz = p.cz + (w + s * 1.0f) * p.az;
-                }
-                done = true;
-            } else {
-                // Re-derive the winner's HitNormal / NextRayOrigin exactly as
-                // they were formed at acceptance (main.cpp:423-429).
-                const float *gsph = reinterpret_cast<const float *>(lds_groups) + 16u * (sidx >> 2) + (sidx & 3u);
-                const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
-                const float cx = sx - p.ox, cy = sy - p.oy, cz = sz - p.oz;
-                const float ipx = p.dx * tmin, ipy = p.dy * tmin, ipz = p.dz * tmin;
-                const float hx = ipx - cx, hy = ipy - cy, hz = ipz - cz;
-                p.ox = p.ox + ipx;
-                p.oy = p.oy + ipy;
-                p.oz = p.oz + ipz;
-                const float4 cs = lds_mats[2u * sidx + 0u];
-                const float4 ei = lds_mats[2u * sidx + 1u];
-                shade(lut, cs, ei, hx, hy, hz, inside, p);
-                p.bounce += 1;
-                done = p.bounce == a.max_bounce;
-            }
-            if (done) {
-                // ---- running-mean blend (main.cpp:484-489)
-                const uint32_t pc = a.prev_count + k;
-                const float inv = k < kFoldTable ? fold[k].x : 1.0f / (float)(pc + 1u);
-                const float ratio = k < kFoldTable ? fold[k].y : (float)pc / (float)(pc + 1u);
-                accx = p.cx * inv + accx * ratio;
-                accy = p.cy * inv + accy * ratio;
-                accz = p.cz * inv + accz * ratio;
-                k += 1;
-                mode = k < a.frames ? 0u : 2u;
-            } else {
-                mode = 1u;
+        }
+        if (P > 1 && owner && valid) {
+            // ---- running-mean blend (main.cpp:484-489) of every finished sample, in order
+            for (;;) {
+                if (folded >= a.frames) break;
+                const float4 r = ring[folded % kRing];
+                if (r.w == 0.0f) break;
+                ring[folded % kRing].w = 0.0f;
+                const uint32_t pc = a.prev_count + folded;
+                const float inv = folded < kFoldTable ? fold[folded].x : 1.0f / (float)(pc + 1u);
+                const float ratio = folded < kFoldTable ? fold[folded].y : (float)pc / (float)(pc + 1u);
+                accx = r.x * inv + accx * ratio;
+                accy = r.y * inv + accy * ratio;
+                accz = r.z * inv + accz * ratio;
+                folded += 1u;
             }
         }
     }
 
-    if (valid && a.frames > 0) {
+    if (valid && owner && a.frames > 0) {
+        const size_t pix = (size_t)ly * a.width + x;
         a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
         a.cur[pix] = to_u8(linear_to_srgb(accx)) | (to_u8(linear_to_srgb(accy)) << 8) |
                      (to_u8(linear_to_srgb(accz)) << 16) | (255u << 24);
@@ -588,12 +652,18 @@ __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(Trac
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
     if (lane == 0 && sum) atomicAdd(a.rays, (unsigned long long)sum);
+    if (a.wave_times && lane == 0) {
+        const uint64_t wid = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4u + wave;
+        a.wave_times[2 * wid + 0] = t_start;
+        a.wave_times[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (a.stats && lane == 0) {
         atomicAdd(a.stats + kStatPriIters, (unsigned long long)st_pri_it);
         atomicAdd(a.stats + kStatPriLanes, (unsigned long long)st_pri_lanes);
         atomicAdd(a.stats + kStatSecIters, (unsigned long long)st_sec_it);
         atomicAdd(a.stats + kStatSecLanes, (unsigned long long)st_sec_lanes);
         atomicAdd(a.stats + kStatPriGroups, (unsigned long long)st_groups);
+        atomicAdd(a.stats + kStatSecHitGroups, (unsigned long long)st_sec_hit);
     }
 }
 
@@ -621,11 +691,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint8_t *src, uint6
 
 }  // namespace rtk
 
-extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream) {
+template <int P>
+static void launch_p(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream) {
+    constexpr uint32_t BW = 2u * rtk::Shape<P>::TW, BH = 2u * rtk::Shape<P>::TH;
     const dim3 block(256);
-    const dim3 grid((a->width + 15u) / 16u, (a->local_rows + 15u) / 16u);
+    const dim3 grid((a->width + BW - 1u) / BW, (a->local_rows + BH - 1u) / BH);
     const size_t lds = rtk_lds_bytes(a->n_groups);
-#define RTK_LAUNCH(S, R, C) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C>), grid, block, lds, stream, *a)
+#define RTK_LAUNCH(S, R, C) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P>), grid, block, lds, stream, *a)
     const int key = (simd ? 4 : 0) | (src == kSrcLds ? 2 : 0) | (cull ? 1 : 0);
     switch (key) {
         case 0: RTK_LAUNCH(false, kSrcSmem, false); break;
@@ -638,6 +710,13 @@ extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull,
         default: RTK_LAUNCH(true, kSrcLds, true); break;
     }
 #undef RTK_LAUNCH
+}
+
+extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
+                                hipStream_t stream) {
+    if (lanes_per_pixel == 4) launch_p<4>(a, simd, src, cull, stream);
+    else if (lanes_per_pixel == 2) launch_p<2>(a, simd, src, cull, stream);
+    else launch_p<1>(a, simd, src, cull, stream);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
