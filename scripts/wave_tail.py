@@ -21,6 +21,7 @@ for _ in range(2):
               frames=S, max_bounce=B, accum_zero=True)
 torch.cuda.synchronize()
 wt = dev.debug_wave_times().astype(np.int64)
+wt = wt[wt[:, 1] > 0]
 t0 = wt[:, 0].min()
 st, en = (wt[:, 0] - t0) / 100.0, (wt[:, 1] - t0) / 100.0  # microseconds
 dur = en - st
@@ -30,8 +31,8 @@ T = en.max()
 for f in np.linspace(0, 1, 21)[:-1]:
     t = f * T
     print(f"t={t:8.0f}us active waves {int(((st <= t) & (en > t)).sum()):6d}")
-gx = (W + 15) // 16
+gx = (W + 7) // 8
 wid = np.arange(len(wt))
 bx, by, w = (wid // 4) % gx, (wid // 4) // gx, wid % 4
 slow = np.argsort(-dur)[:10]
-print("slowest waves (tile x,y):", [(int(bx[i] * 16 + (w[i] & 1) * 8), int(by[i] * 16 + (w[i] >> 1) * 8), int(dur[i])) for i in slow])
+print("slowest waves (tile x,y):", [(int(bx[i] * 8 + (w[i] & 1) * 4), int(by[i] * 8 + (w[i] >> 1) * 4), int(dur[i])) for i in slow])

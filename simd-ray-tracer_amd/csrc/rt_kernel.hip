@@ -109,8 +109,10 @@ __device__ __forceinline__ float reflectance(float cos_t, float eta) {  // main.
     return __builtin_fmaf(1.0f - r0, r1, r0);  // contracted by the reference's -mfma build
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 struct Sample {
-    float ox, oy, oz, dx, dy, dz;
+    f2 rx, ry, rz;     // {origin, direction} per axis (the packed pair test reads them in place)
     float ax, ay, az;  // attenuation
     float cx, cy, cz;  // output colour
     uint64_t rng;
@@ -129,13 +131,14 @@ __device__ __forceinline__ void start_sample(const TraceArgs &a, uint32_t x, uin
     const float px = (a.film_center[0] + kx * a.cam_x[0]) + ky * a.cam_y[0];
     const float py = (a.film_center[1] + kx * a.cam_x[1]) + ky * a.cam_y[1];
     const float pz = (a.film_center[2] + kx * a.cam_x[2]) + ky * a.cam_y[2];
-    p.ox = a.cam_pos[0];
-    p.oy = a.cam_pos[1];
-    p.oz = a.cam_pos[2];
-    p.dx = px - p.ox;
-    p.dy = py - p.oy;
-    p.dz = pz - p.oz;
-    normalize(p.dx, p.dy, p.dz);
+    p.rx.x = a.cam_pos[0];
+    p.ry.x = a.cam_pos[1];
+    p.rz.x = a.cam_pos[2];
+    float dx = px - p.rx.x, dy = py - p.ry.x, dz = pz - p.rz.x;
+    normalize(dx, dy, dz);
+    p.rx.y = dx;
+    p.ry.y = dy;
+    p.rz.y = dz;
     p.ax = p.ay = p.az = 1.0f;
     p.cx = p.cy = p.cz = 0.0f;
     p.bounce = 0;
@@ -152,8 +155,8 @@ __device__ __forceinline__ void shade(const float *lut, float4 col_spec, float4 
     p.az = p.az * col_spec.z;
     float nx = hx, ny = hy, nz = hz;
     normalize(nx, ny, nz);
-    const float k2 = 2.0f * dot3(p.dx, p.dy, p.dz, nx, ny, nz);
-    const float bx = p.dx - k2 * nx, by = p.dy - k2 * ny, bz = p.dz - k2 * nz;  // PureBounce
+    const float k2 = 2.0f * dot3(p.rx.y, p.ry.y, p.rz.y, nx, ny, nz);
+    const float bx = p.rx.y - k2 * nx, by = p.ry.y - k2 * ny, bz = p.rz.y - k2 * nz;  // PureBounce
     if (inside) {
         nx = -nx;
         ny = -ny;
@@ -172,32 +175,35 @@ __device__ __forceinline__ void shade(const float *lut, float4 col_spec, float4 
         rz = keep ? rz * inv : 0.0f;
         const float s = col_spec.w;
         const float om = 1.0f - s;
-        p.dx = om * (nx + rx) + s * bx;
-        p.dy = om * (ny + ry) + s * by;
-        p.dz = om * (nz + rz) + s * bz;
-        normalize(p.dx, p.dy, p.dz);
+        float dx = om * (nx + rx) + s * bx;
+        float dy = om * (ny + ry) + s * by;
+        float dz = om * (nz + rz) + s * bz;
+        normalize(dx, dy, dz);
+        p.rx.y = dx;
+        p.ry.y = dy;
+        p.rz.y = dz;
     } else {
         const float eta = inside ? ior : 1.0f / ior;
-        const float dd = dot3(-p.dx, -p.dy, -p.dz, nx, ny, nz);
+        const float dd = dot3(-p.rx.y, -p.ry.y, -p.rz.y, nx, ny, nz);
         const float cos_t = dd < 1.0f ? dd : 1.0f;  // _mm_min_ss
         const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
         const bool cant = eta * sin_t > 1.0f;
-        const float qx = eta * (p.dx + cos_t * nx);
-        const float qy = eta * (p.dy + cos_t * ny);
-        const float qz = eta * (p.dz + cos_t * nz);
+        const float qx = eta * (p.rx.y + cos_t * nx);
+        const float qy = eta * (p.ry.y + cos_t * ny);
+        const float qz = eta * (p.rz.y + cos_t * nz);
         const float q = -__builtin_sqrtf(__builtin_fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
         float rx = qx + q * nx, ry = qy + q * ny, rz = qz + q * nz;
         normalize(rx, ry, rz);
         bool refl = cant;
         if (!refl) refl = reflectance(cos_t, eta) > rand_float(p.rng, 0.0f, kInvRange1);
         if (refl && !inside) {
-            p.dx = bx;
-            p.dy = by;
-            p.dz = bz;
+            p.rx.y = bx;
+            p.ry.y = by;
+            p.rz.y = bz;
         } else {
-            p.dx = rx;
-            p.dy = ry;
-            p.dz = rz;
+            p.rx.y = rx;
+            p.ry.y = ry;
+            p.rz.y = rz;
         }
     }
 }
@@ -236,9 +242,9 @@ __device__ __forceinline__ Group load_group(const TraceArgs &a, const float4 *ld
 
 // The shared part of one sphere test: T, |C - D*T|^2 (main.cpp:401-407).
 __device__ __forceinline__ void sphere_core(const Sample &p, float sx, float sy, float sz, float &T, float &dist) {
-    const float cx = sx - p.ox, cy = sy - p.oy, cz = sz - p.oz;
-    T = dot3(cx, cy, cz, p.dx, p.dy, p.dz);
-    const float qx = cx - p.dx * T, qy = cy - p.dy * T, qz = cz - p.dz * T;
+    const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
+    T = dot3(cx, cy, cz, p.rx.y, p.ry.y, p.rz.y);
+    const float qx = cx - p.rx.y * T, qy = cy - p.ry.y * T, qz = cz - p.rz.y * T;
     dist = dot3(qx, qy, qz, qx, qy, qz);
 }
 
@@ -256,10 +262,6 @@ __device__ __forceinline__ void hit_reset(Hit &h) {
     h.g0 = h.g1 = h.g2 = h.g3 = 0;
     h.ins = 0;
 }
-
-struct Ray {  // passed by value so no callee ever loads the path state through a pointer
-    float ox, oy, oz, dx, dy, dz;
-};
 
 // Exact intersection of one candidate sphere (main.cpp:413-429 / 561-578),
 // given its T and |C - D*T|^2 from the packed distance test.
@@ -290,25 +292,50 @@ __device__ __forceinline__ void candidate(Hit &h, uint32_t g, float T, float dis
     }
 }
 
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 // T and |C - D*T|^2 for two spheres of a group at once: every f32 op of
 // main.cpp:401-407 becomes one packed v_pk_{add,mul}_f32 over the pair (same
 // IEEE rounding per element; a packed op issues at the cost of a scalar one
 // on gfx950, so this halves the sphere loop's VALU instructions).
-__device__ __forceinline__ f2 pair_dist(const Ray r, f2 sx, f2 sy, f2 sz, f2 &T) {
-    const f2 ox = {r.ox, r.ox}, oy = {r.oy, r.oy}, oz = {r.oz, r.oz};
-    const f2 dx = {r.dx, r.dx}, dy = {r.dy, r.dy}, dz = {r.dz, r.dz};
-    const f2 cx = sx - ox, cy = sy - oy, cz = sz - oz;
-    T = (cx * dx + cy * dy) + cz * dz;
-    const f2 qx = cx - dx * T, qy = cy - dy * T, qz = cz - dz * T;
-    return (qx * qx + qy * qy) + qz * qz;
+// The ray as three {origin, direction} register pairs: a packed op can then
+// broadcast either half to both lanes with op_sel / op_sel_hi, so the pair
+// test needs no duplicated (splat) copies of the ray.
+struct RayPk {
+    f2 x, y, z;  // {o, d} per axis
+};
+
+__device__ __forceinline__ f2 pair_dist(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 &T) {
+    f2 cx, cy, cz, t, d;
+    // c = s - o ; T = (cx*dx + cy*dy) + cz*dz ; q = c - d*T (in c) ;
+    // dist = (qx*qx + qy*qy) + qz*qz  -- op for op the reference's f32 sequence
+    asm("v_pk_add_f32 %[cx], %[sx], %[rx] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[cy], %[sy], %[ry] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[cz], %[sz], %[rz] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[t], %[cx], %[rx] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_mul_f32 %[d], %[cy], %[ry] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[T], %[t], %[d]\n\t"
+        "v_pk_mul_f32 %[t], %[cz], %[rz] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[T], %[T], %[t]\n\t"
+        "v_pk_mul_f32 %[t], %[rx], %[T] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[cx], %[cx], %[t] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[t], %[ry], %[T] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[cy], %[cy], %[t] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[t], %[rz], %[T] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[cz], %[cz], %[t] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[d], %[cx], %[cx]\n\t"
+        "v_pk_mul_f32 %[t], %[cy], %[cy]\n\t"
+        "v_pk_add_f32 %[d], %[d], %[t]\n\t"
+        "v_pk_mul_f32 %[t], %[cz], %[cz]\n\t"
+        "v_pk_add_f32 %[d], %[d], %[t]"
+        : [cx] "=&v"(cx), [cy] "=&v"(cy), [cz] "=&v"(cz), [t] "=&v"(t), [T] "=&v"(T), [d] "=&v"(d)
+        : [sx] "s"(sx), [sy] "s"(sy), [sz] "s"(sz), [rx] "v"(r.x), [ry] "v"(r.y), [rz] "v"(r.z));
+    return d;
 }
 
 // All four spheres of group g; one wave-level branch per group, nested
 // branches only for the (rare) lanes that pass the distance test.
 template <bool SIMD>
-__device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const Ray p, Hit &h,
+__device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const RayPk &p, Hit &h,
                                            uint32_t *hit_groups = nullptr) {
     f2 T01, T23;
     const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
@@ -408,9 +435,9 @@ constexpr int kMaxMaskWords = (kMaxLdsGroups + 63) / 64;
 constexpr uint32_t kFoldTable = 256;
 constexpr uint32_t kRing = 8;  // per-pixel out-of-order sample slots (LDS)
 
-#ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) for the trace kernel
-#define RTK_MIN_WAVES_PER_SIMD 1
-#endif
+#ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) of the production (SMEM) kernels;
+#define RTK_MIN_WAVES_PER_SIMD 6   // 6 waves = 80 VGPRs: measured best on C2 (w1 55.2k, w6 57.7k,
+#endif                             // w7 57.6k, w8 56.0k Mrays/s; w7/w8 spill)
 
 // Work shape.  A wave owns a small pixel tile and P lanes per pixel: lane
 // j of a pixel traces that pixel's samples k = j, j+P, j+2P, ... (any order
@@ -428,7 +455,7 @@ struct Shape {
 };
 
 template <bool SIMD, int SRC, bool CULL, int P>
-__global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(TraceArgs a) {
+__global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) void trace_kernel(TraceArgs a) {
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
     extern __shared__ float4 smem[];
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
@@ -531,7 +558,7 @@ __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(Trac
                     nrays += 1;
                     Hit h;
                     hit_reset(h);
-                    const Ray ray = {p.ox, p.oy, p.oz, p.dx, p.dy, p.dz};
+                    const RayPk ray = {p.rx, p.ry, p.rz};
                     if (CULL && !do_sec) {
                         for (uint32_t w = 0; w < n_words; ++w) {
                             uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
@@ -574,7 +601,7 @@ __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(Trac
                     }
                     if (tmin == kFMax) {
                         if (a.use_sky) {  // main.cpp:434-438
-                            const float s = (p.dy + 1.0f) * 0.5f;
+                            const float s = (p.ry.y + 1.0f) * 0.5f;
                             const float w = (1.0f - s) * 1.0f;
                             p.cx = p.cx + (w + s * 0.5f) * p.ax;
                             p.cy = p.cy + (w + s * 0.7f) * p.ay;
@@ -586,12 +613,12 @@ __global__ __launch_bounds__(256, RTK_MIN_WAVES_PER_SIMD) void trace_kernel(Trac
                         // they were formed at acceptance (main.cpp:423-429).
                         const float *gsph = reinterpret_cast<const float *>(lds_groups) + 16u * (sidx >> 2) + (sidx & 3u);
                         const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
-                        const float cx = sx - p.ox, cy = sy - p.oy, cz = sz - p.oz;
-                        const float ipx = p.dx * tmin, ipy = p.dy * tmin, ipz = p.dz * tmin;
+                        const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
+                        const float ipx = p.rx.y * tmin, ipy = p.ry.y * tmin, ipz = p.rz.y * tmin;
                         const float hx = ipx - cx, hy = ipy - cy, hz = ipz - cz;
-                        p.ox = p.ox + ipx;
-                        p.oy = p.oy + ipy;
-                        p.oz = p.oz + ipz;
+                        p.rx.x = p.rx.x + ipx;
+                        p.ry.x = p.ry.x + ipy;
+                        p.rz.x = p.rz.x + ipz;
                         const float4 cs = lds_mats[2u * sidx + 0u];
                         const float4 ei = lds_mats[2u * sidx + 1u];
                         shade(lut, cs, ei, hx, hy, hz, inside, p);
