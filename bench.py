@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[1], "C2"): 1920x1080, 256 spp, 64 spheres
 that scene's default camera), 8 bounces, per-(pixel, frame) PCG seeds.
 One step = one complete 256-spp render of the frame: every pixel's 256
 progressive frames folded into the running mean and the sRGB RGBA8 stored;
-for N > 1 GPUs the frame is dealt out in interleaved 32-row bands (one rank
+for N > 1 GPUs the frame is dealt out in interleaved 8-row bands (one rank
 per GPU) and gathered to rank 0 over RCCL, then assembled (strong scaling:
 the total work per step is fixed).  Rays = bounce segments counted as the
 reference counts them (main.cpp:390).
@@ -26,9 +26,11 @@ ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 # MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md, chip table):
-# 256 CUs x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T f32 VALU ops/s (one add/mul/
-# cmp per lane per cycle; FMA is not usable on this path: every op must round
-# separately to match the reference).  HBM3E 8 TB/s.
+# a SIMD retires 16 f32 lanes/clk (a wave64 VALU op every 4 clk), 32 with
+# packed v_pk_{add,mul}_f32: 256 CUs x 4 SIMDs x 32 x 2.4 GHz = 78.6 T f32
+# add/mul ops/s (the 157 TFLOP/s spec figure counts an FMA as 2; the path
+# cannot fuse: every op must round separately to match the reference).
+# HBM3E 8 TB/s.
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 
@@ -51,6 +53,7 @@ def parse():
     p.add_argument("--scalar", action="store_true", help="RenderTileScalar rules instead of RenderTile")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--band-rows", type=int, default=8, help="rows per interleaved band (multiple of 8)")
     return p.parse_args()
 
 
@@ -80,6 +83,20 @@ def cpu_baseline(args, n_rays_gpu_step: int):
                       f"RenderTile restatement, pixel seeds)"}
 
 
+def pmc_record(workload: str):
+    """The newest committed rocprofv3 --pmc record of this workload
+    (profiles/rNN_*_pmc.json, written by scripts/pmc_to_json.py)."""
+    for f in sorted((ROOT / "profiles").glob("r*_pmc.json"), reverse=True):
+        try:
+            rec = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        if rec.get("workload") == workload:
+            rec["file"] = f"profiles/{f.name}"
+            return rec
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -102,7 +119,7 @@ def main():
     cam = rt.camera_setup(scene, W, H)
     dev = rt.Device(local)
     dev.upload_scene(scene)
-    band_rows = 32
+    band_rows = args.band_rows
     rows = [rt.band_local_rows(H, band_rows, world, r) for r in range(world)]
     maxr = max(rows)
     cur = torch.zeros(maxr * W, dtype=torch.int32, device="cuda")
@@ -160,6 +177,22 @@ def main():
         achieved = ops / (kern_ms / 1e3) / 1e12
         fb_bytes = rows[0] * W * (16 + 4)  # accumulation + RGBA8 written once per launch
         hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
+        workload = f"C2: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
+        pmc = pmc_record(workload)
+        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                "traffic": round(pmc["hbm_bytes_per_dispatch"]) if pmc and "hbm_bytes_per_dispatch" in pmc else None,
+                "kernel": "trace_kernel<SIMD,SMEM,CULL,4>", "kernel_ms": round(kern_ms, 3),
+                "work_per_launch": f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d, brute force)",
+                "note": "algorithmic ops count every sphere for every segment; the kernel culls sphere groups "
+                        "for primary rays exactly, so it executes fewer ops and frac may exceed 1. The "
+                        "executed-instruction bound is 'issue' (PMC).",
+                "hbm": {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}}
+        if pmc:
+            roof["issue"] = {k: round(pmc[k], 4) for k in ("valu_issue_frac", "valu_lane_utilisation") if k in pmc}
+            roof["issue"]["source"] = pmc["file"]
+            roof["traffic_source"] = pmc["file"] + " (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
         line = {
             "metric": "Mrays/sec at 1920x1080, 256spp, 8 bounces, 64 spheres",
             "value": round(value, 1),
@@ -174,18 +207,12 @@ def main():
             "dtype": "f32",
             "data": "synthetic (first 64 spheres of the reference's Floating Spheres scene, default camera, "
                     "per-(pixel,frame) PCG seeds)",
-            "config": {"workload": f"C2: {W}x{H}, {S} spp, {N} spheres, {B} bounces, "
-                                   f"{'scalar' if args.scalar else 'SIMD'} rules",
+            "config": {"workload": workload,
                        "width": W, "height": H, "spp": S, "spheres": N, "bounces": B,
-                       "parallelism": f"{world} GPU x interleaved 32-row bands" + (" + RCCL gather" if world > 1 else ""),
+                       "parallelism": f"{world} GPU x interleaved {band_rows}-row bands" +
+                                      (" + RCCL gather" if world > 1 else ""),
                        "rays_per_step": int(rays_per_step.item())},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 1),
-                         "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
-                         "kernel": "trace_kernel<SIMD>", "kernel_ms": round(kern_ms, 3),
-                         "work_per_launch": f"{rays_local} segments x (21*{N}+70) f32 ops",
-                         "hbm": {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(hbm_achieved / HBM_PEAK_GBS, 6),
-                                 "bytes_per_launch": fb_bytes}},
+            "roofline": roof,
         }
         stats = dev.debug_stats()
         if stats:

@@ -181,7 +181,7 @@ typedef struct rt_trace_desc {
     uint32_t MaxBounce;       /* the reference literal is 5 (main.cpp:387)       */
     uint32_t EnableSIMD;      /* 1 RenderTile rules, 0 RenderTileScalar rules    */
     uint32_t SeedMode;        /* RT_SEED_PIXEL                                   */
-    uint32_t BandRows;        /* row-band height for multi-GPU dispatch (32)     */
+    uint32_t BandRows;        /* row-band height, a multiple of 8 (bench: 8)     */
     uint32_t BandCount;       /* bands are dealt round-robin over BandCount GPUs */
     uint32_t BandIndex;       /* this GPU's residue                              */
     uint32_t Flags;           /* RT_FLAG_*                                       */
