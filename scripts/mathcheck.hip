@@ -1,0 +1,103 @@
+// GPU verification of the short exact-rounding sequences considered for the
+// trace kernel, against the compiler's IEEE sequences (-ffp-contract=off):
+//   rcp:  y = RN(1/b) from v_rcp_f32 + one Newton step       (exhaustive mantissas x exponent range)
+//   sqrt: RN(sqrt(x)) from v_sqrt_f32 + +-1ulp residual fix   (exhaustive mantissas x exponent range)
+//   div:  RN(a/b) = fma(r, y, q0), q0 = a*y, r = fma(-q0, b, a), y = RN(1/b)  (random + edge pairs)
+// Prints mismatch counts and the first few mismatching inputs.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+__device__ __forceinline__ float rcp_fast(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y0, 1.0f);
+    return __builtin_fmaf(e, y0, y0);
+}
+__device__ __forceinline__ float sqrt_fast(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = s;
+    if (__builtin_fmaf(-sm, s, x) <= 0.0f) r = sm;
+    if (__builtin_fmaf(-sp, s, x) > 0.0f) r = sp;
+    return r;
+}
+__device__ __forceinline__ float div_fast(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = __builtin_fmaf(-q0, b, a);
+    return __builtin_fmaf(r, y, q0);
+}
+
+__device__ void report(unsigned long long *cnt, uint32_t *bad, uint32_t a, uint32_t b) {
+    const unsigned long long i = atomicAdd(cnt, 1ull);
+    if (i < 8) { bad[2 * i] = a; bad[2 * i + 1] = b; }
+}
+
+// mode 0: rcp, 1: sqrt over u = (e0 + blockIdx.y) << 23 | mantissa
+__global__ void k_unary(int mode, int e0, unsigned long long *cnt, uint32_t *bad) {
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= (1u << 23)) return;
+    const uint32_t u = ((uint32_t)(e0 + (int)blockIdx.y) << 23) | m;
+    const float x = __uint_as_float(u);
+    float got, want;
+    if (mode == 0) { got = rcp_fast(x); want = 1.0f / x; }
+    else { got = sqrt_fast(x); want = __builtin_sqrtf(x); }
+    if (__float_as_uint(got) != __float_as_uint(want)) report(cnt, bad, u, 0);
+}
+
+__device__ __forceinline__ uint32_t pcg(uint64_t &s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ULL + 1442695040888963407ULL;
+    const uint32_t v = (uint32_t)(old >> 32) ^ (uint32_t)old;
+    return __builtin_amdgcn_alignbit(v, v, (uint32_t)(old >> 59));
+}
+
+// division pairs: b from an exponent window [eb0, eb0+16), a anywhere in
+// [ea0, ea0+64) exponents, random mantissas (plus every 16th pair with b's
+// mantissa near 1 or 2 and a's near a multiple of b)
+__global__ void k_div(uint64_t seed, int iters, int ea0, int eb0, unsigned long long *cnt, uint32_t *bad) {
+    uint64_t s = seed ^ ((uint64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 0x9E3779B97F4A7C15ULL);
+    for (int it = 0; it < iters; ++it) {
+        const uint32_t r0 = pcg(s), r1 = pcg(s), r2 = pcg(s);
+        uint32_t mb = r1 & 0x7FFFFFu;
+        if ((r2 & 15u) == 0) mb = (r2 & 16u) ? (r1 & 0xFFu) : (0x7FFFFFu - (r1 & 0xFFu));
+        const uint32_t ub = ((uint32_t)(eb0 + (int)((r2 >> 8) & 15u)) << 23) | mb;
+        const float b = __uint_as_float(ub);
+        uint32_t ua = ((uint32_t)(ea0 + (int)((r2 >> 12) & 63u)) << 23) | (r0 & 0x7FFFFFu);
+        if ((r2 & 0xF0000u) == 0) {  // a close to k*b: quotient near a representable value
+            const float k = (float)((r0 >> 9) | 1u);
+            ua = __float_as_uint(k * b) + ((r2 >> 24) & 3u) - 1u;
+        }
+        if (r2 >> 31) ua |= 0x80000000u;
+        const float a = __uint_as_float(ua);
+        const float y = 1.0f / b;
+        const float got = div_fast(a, b, y), want = a / b;
+        if (__float_as_uint(got) != __float_as_uint(want) && !(got != got && want != want)) report(cnt, bad, ua, ub);
+    }
+}
+
+int main() {
+    unsigned long long *cnt;
+    uint32_t *bad;
+    (void)hipMalloc(&cnt, 8);
+    (void)hipMalloc(&bad, 64);
+    auto run = [&](const char *name, auto launch) {
+        (void)hipMemset(cnt, 0, 8);
+        (void)hipMemset(bad, 0, 64);
+        launch();
+        (void)hipDeviceSynchronize();
+        unsigned long long c;
+        uint32_t h[16];
+        (void)hipMemcpy(&c, cnt, 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(h, bad, 64, hipMemcpyDeviceToHost);
+        printf("%-34s mismatches %llu", name, c);
+        for (int i = 0; i < 8 && i < (int)c; ++i) printf("  [%08x %08x]", h[2 * i], h[2 * i + 1]);
+        printf("\n");
+    };
+    // exponents 127-40 .. 127+40: x in [2^-40, 2^40)
+    run("rcp  rcp+Newton, 2^-40..2^40", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 80), dim3(256), 0, 0, 0, 87, cnt, bad); });
+    run("sqrt v_sqrt+fix, 2^-60..2^60", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 1, 67, cnt, bad); });
+    // b in [2^-8, 2^8), a in [2^-40, 2^24): quotients 2^-48 .. 2^32 (normal)
+    for (int rep = 0; rep < 4; ++rep)
+        run("div  q0+fma, b 2^-8..2^8", [&] { hipLaunchKernelGGL(k_div, dim3(16384), dim3(256), 0, 0, 0x1234567ull + rep, 512, 87, 119, cnt, bad); });
+    return 0;
+}

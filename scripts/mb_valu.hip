@@ -2,6 +2,7 @@
 //   mode 0: v_mul_f32, 8 independent chains / wave   mode 1: v_pk_mul_f32, 8 chains
 //   mode 2: v_fma_f32, 8 chains                         mode 3: v_mul_f32, ONE dependent chain
 //   mode 4: v_mul_f32, 2 chains                         mode 5: 8 chains + a uniform s_cbranch per 8 ops
+//   mode 6: v_pk_fma_f32, 8 chains                      mode 7: v_pk_mul_f32, 4 chains (dependent pairs)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 typedef float float2_t __attribute__((ext_vector_type(2)));
@@ -19,6 +20,12 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, float s) {
         } else if (MODE == 2) {
             a0 = __builtin_fmaf(a0, s, s); a1 = __builtin_fmaf(a1, s, s); a2 = __builtin_fmaf(a2, s, s); a3 = __builtin_fmaf(a3, s, s);
             a4 = __builtin_fmaf(a4, s, s); a5 = __builtin_fmaf(a5, s, s); a6 = __builtin_fmaf(a6, s, s); a7 = __builtin_fmaf(a7, s, s);
+        } else if (MODE == 6) {
+#define PKFMA(p) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(p) : "v"(ss))
+            PKFMA(p0); PKFMA(p1); PKFMA(p2); PKFMA(p3); PKFMA(p4); PKFMA(p5); PKFMA(p6); PKFMA(p7);
+        } else if (MODE == 7) {
+#define PKMUL(p) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(p) : "v"(ss))
+            PKMUL(p0); PKMUL(p1); PKMUL(p2); PKMUL(p3); PKMUL(p0); PKMUL(p1); PKMUL(p2); PKMUL(p3);
         } else if (MODE == 3) {
             a0 *= s; a0 *= s; a0 *= s; a0 *= s; a0 *= s; a0 *= s; a0 *= s; a0 *= s;
         } else {
@@ -35,8 +42,8 @@ int main(int argc, char** argv) {
     int blocks = argc > 2 ? atoi(argv[2]) : 2048;
     int iters = argc > 3 ? atoi(argv[3]) : 20000;
     int only = argc > 4 ? atoi(argv[4]) : -1;
-    const char* names[6] = {"mul x8 chains", "pk_mul x8 chains", "fma x8 chains", "mul 1 chain", "mul 2 chains", "mul x8 + branch"};
-    for (int m = 0; m < 6; ++m) {
+    const char* names[8] = {"mul x8 chains", "pk_mul x8 chains", "fma x8 chains", "mul 1 chain", "mul 2 chains", "mul x8 + branch", "pk_fma x8 chains", "pk_mul x4 chains"};
+    for (int m = 0; m < 8; ++m) {
         if (only >= 0 && m != only) continue;
         for (int rep = 0; rep < 2; ++rep) {
         (void)hipEventRecord(a);
@@ -48,6 +55,8 @@ int main(int argc, char** argv) {
             case 3: hipLaunchKernelGGL(k<3>, g, t, 0, 0, out, iters, 0.999f); break;
             case 4: hipLaunchKernelGGL(k<4>, g, t, 0, 0, out, iters, 0.999f); break;
             case 5: hipLaunchKernelGGL(k<5>, g, t, 0, 0, out, iters, 0.999f); break;
+            case 6: hipLaunchKernelGGL(k<6>, g, t, 0, 0, out, iters, 0.999f); break;
+            case 7: hipLaunchKernelGGL(k<7>, g, t, 0, 0, out, iters, 0.999f); break;
         }
         (void)hipEventRecord(b); (void)hipEventSynchronize(b);
         float ms; (void)hipEventElapsedTime(&ms, a, b);

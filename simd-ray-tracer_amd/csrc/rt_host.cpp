@@ -6,6 +6,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "rt_kernel.h"
@@ -27,6 +29,8 @@ struct rt_device {
     int src = kSrcSmem;
     int cull = 1;
     uint32_t sec_threshold = 16;
+    int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
+    uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
     int lanes_per_pixel = 4;
     unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
     unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
@@ -72,6 +76,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (cull && cull[0] == '0') d->cull = 0;
     const char *thr = getenv("RT_SEC_THRESHOLD");
     if (thr) d->sec_threshold = (uint32_t)atoi(thr);
+    const char *pf = getenv("RT_PREFILTER");  // secondary-ray prefilter: 0 off, 1 on, unset = per-scene auto
+    if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -117,14 +123,15 @@ static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, co
         (void)hipFree(d->d_mats[rs]);
         d->d_groups[rs] = nullptr;
         d->d_mats[rs] = nullptr;
-        // +1 padding group: the kernel prefetches group g+1 while testing g
-        if (hipMalloc(&d->d_groups[rs], (size_t)(n_groups + 1) * 64) != hipSuccess ||
+        // +2 padding groups: the kernel's loops prefetch up to group g+2 while testing g
+        if (hipMalloc(&d->d_groups[rs], (size_t)(n_groups + 2) * kGroupF4 * 16) != hipSuccess ||
             hipMalloc(&d->d_mats[rs], (size_t)n_groups * 128) != hipSuccess)
             return fail(RT_ENOMEM, "rt_scene_upload: device allocation failed");
         d->cap_groups[rs] = n_groups;
     }
-    HIP_OK(hipMemsetAsync(d->d_groups[rs] + 4 * (size_t)n_groups, 0, 64, d->stream));
-    HIP_OK(hipMemcpyAsync(d->d_groups[rs], groups.data(), (size_t)n_groups * 64, hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemsetAsync(d->d_groups[rs] + kGroupF4 * (size_t)n_groups, 0, 2 * kGroupF4 * 16, d->stream));
+    HIP_OK(hipMemcpyAsync(d->d_groups[rs], groups.data(), (size_t)n_groups * kGroupF4 * 16, hipMemcpyHostToDevice,
+                          d->stream));
     HIP_OK(hipMemcpyAsync(d->d_mats[rs], mats.data(), (size_t)n_groups * 128, hipMemcpyHostToDevice, d->stream));
     d->n_groups[rs] = n_groups;
     return RT_OK;
@@ -141,6 +148,48 @@ static void put_material(float *dst, const rt_material &m) {
     dst[7] = m.IndexOfRefraction;
 }
 
+// Prefilter thresholds r2p (row 4 of each group) for the secondary-ray
+// sphere loop (rt_kernel.hip, pair_prefilter).  Secondary origins are hit
+// points, i.e. lie within |r_i| of a hittable sphere centre s_i, so
+//   M_j = (max_i |s_i - s_j| + |r_i|)^2   (with slack for origin rounding)
+// bounds |C|^2 for sphere j, and r2p_j = r^2_j + M_j (32u + 1.01K) rounded
+// up (u = 2^-24, K = 2^-16) exceeds the prefilter's error bound.  Spheres
+// that can never pass the exact test (SIMD r^2 <= 0, scalar padding) get
+// -inf: never flagged.  Returns whether the prefilter pays for this scene
+// (thresholds not far above r^2 on average).
+static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd) {
+    std::vector<uint32_t> hit;
+    for (uint32_t s = 0; s < 4u * n_groups; ++s) {
+        const float r2 = gv[(s / 4u) * 4u * kGroupF4 + 12u + s % 4u];
+        if (simd ? r2 > 0.0f : r2 >= 0.0f) hit.push_back(s);
+    }
+    double ratio = 0.0;
+    uint32_t n_ratio = 0;
+    for (uint32_t j = 0; j < 4u * n_groups; ++j) {
+        const uint32_t gj = (j / 4u) * 4u * kGroupF4, lj = j % 4u;
+        const float r2 = gv[gj + 12u + lj];
+        float &r2p = gv[gj + 16u + lj];
+        if (!(simd ? r2 > 0.0f : r2 >= 0.0f) || !std::isfinite(r2)) {
+            r2p = -INFINITY;
+            continue;
+        }
+        double reach = 0.0;
+        for (uint32_t i : hit) {
+            const uint32_t gi = (i / 4u) * 4u * kGroupF4, li = i % 4u;
+            const double dx = (double)gv[gi + li] - gv[gj + lj], dy = (double)gv[gi + 4u + li] - gv[gj + 4u + lj],
+                         dz = (double)gv[gi + 8u + li] - gv[gj + 8u + lj];
+            const double ri = std::sqrt((double)gv[gi + 12u + li]);
+            reach = std::max(reach, std::sqrt(dx * dx + dy * dy + dz * dz) + ri);
+        }
+        const double m = (reach * 1.001 + 1e-3) * (reach * 1.001 + 1e-3);
+        const double e = m * (32.0 * 0x1p-24 + 1.01 * 0x1p-16);
+        r2p = std::nextafter((float)((double)r2 + e), INFINITY);
+        ratio += std::min(e / std::max((double)r2, 1e-30), 10.0);
+        n_ratio += 1;
+    }
+    return n_ratio > 0 && ratio / n_ratio < 0.5;
+}
+
 extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
     const uint32_t ng = scene->SIMDSpheres.Count;
@@ -155,35 +204,39 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     {
         const rt_sphere_group *g = (const rt_sphere_group *)scene->SIMDSpheres.Data;
         const rt_material *m = (const rt_material *)scene->Materials.Data;
-        std::vector<float> gv((size_t)ng * 16), mv((size_t)ng * 32, 0.0f);
+        std::vector<float> gv((size_t)ng * 4 * kGroupF4), mv((size_t)ng * 32, 0.0f);
         for (uint32_t i = 0; i < ng; ++i) {
             for (int l = 0; l < 4; ++l) {
-                gv[i * 16 + 0 + l] = g[i].X[l];
-                gv[i * 16 + 4 + l] = g[i].Y[l];
-                gv[i * 16 + 8 + l] = g[i].Z[l];
-                gv[i * 16 + 12 + l] = g[i].Radii[l] * g[i].Radii[l];
+                gv[i * 4 * kGroupF4 + 0 + l] = g[i].X[l];
+                gv[i * 4 * kGroupF4 + 4 + l] = g[i].Y[l];
+                gv[i * 4 * kGroupF4 + 8 + l] = g[i].Z[l];
+                gv[i * 4 * kGroupF4 + 12 + l] = g[i].Radii[l] * g[i].Radii[l];
                 const uint32_t s = 4u * i + (uint32_t)l;
                 if (s < scene->Materials.Count) put_material(&mv[(size_t)s * 8], m[s]);
             }
         }
+        const bool pays = prefilter_rows(gv, ng, true);
+        d->prefilter[0] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
         int rc = upload_set(d, 0, gv, mv, ng);
         if (rc) return rc;
     }
     // Scalar rules: ScalarSpheres[s].Position/Radius/Material (main.cpp:547-590).
     {
         const rt_scalar_sphere *s = (const rt_scalar_sphere *)scene->ScalarSpheres.Data;
-        std::vector<float> gv((size_t)ngs * 16, 0.0f), mv((size_t)ngs * 32, 0.0f);
+        std::vector<float> gv((size_t)ngs * 4 * kGroupF4, 0.0f), mv((size_t)ngs * 32, 0.0f);
         for (uint32_t i = 0; i < ns; ++i) {
             const uint32_t gi = i / 4u, l = i % 4u;
-            gv[gi * 16 + 0 + l] = s[i].Position.x;
-            gv[gi * 16 + 4 + l] = s[i].Position.y;
-            gv[gi * 16 + 8 + l] = s[i].Position.z;
-            gv[gi * 16 + 12 + l] = s[i].Radius * s[i].Radius;
+            gv[gi * 4 * kGroupF4 + 0 + l] = s[i].Position.x;
+            gv[gi * 4 * kGroupF4 + 4 + l] = s[i].Position.y;
+            gv[gi * 4 * kGroupF4 + 8 + l] = s[i].Position.z;
+            gv[gi * 4 * kGroupF4 + 12 + l] = s[i].Radius * s[i].Radius;
             put_material(&mv[(size_t)i * 8], s[i].Material);
         }
         // Padding lanes of the scalar packing are skipped by the kernel's
         // s < n_spheres test (the scalar loop runs to Count, main.cpp:547).
-        for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 16 + 12 + (i % 4u)] = -__builtin_inff();
+        for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 4 * kGroupF4 + 12 + (i % 4u)] = -__builtin_inff();
+        const bool pays = prefilter_rows(gv, ngs, false);
+        d->prefilter[1] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
         int rc = upload_set(d, 1, gv, mv, ngs);
         if (rc) return rc;
     }
@@ -242,6 +295,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.band_count = band_count;
     a.band_index = desc->BandIndex;
     a.sec_threshold = d->sec_threshold;
+    a.prefilter = d->prefilter[rs];
     a.stats = d->d_stats;
     if (d->want_wave_times) {
         const size_t waves = (size_t)((desc->Width + 7u) / 8u) * ((local_rows + 7u) / 8u) * 4u * 4u;  // >= any shape

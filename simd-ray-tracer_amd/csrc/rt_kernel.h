@@ -6,10 +6,12 @@
 #include <stdint.h>
 
 enum { kSrcSmem = 0, kSrcLds = 1 };  // where the sphere loop reads its groups
+constexpr uint32_t kGroupF4 = 5;      // float4 rows per sphere group
 enum { kFlagAccumZero = 1 };
 
 // HBM layout of an uploaded scene (per rule set):
-//   groups    : n_groups x 4 float4 = {x[4]}, {y[4]}, {z[4]}, {r*r[4]}   (64 B/group)
+//   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r*r[4]}, {r2p[4]}  (80 B/group)
+//               r2p = prefilter threshold of the secondary-ray sphere loop (rt_host.cpp)
 //   materials : 4*n_groups x 2 float4 = {Color.xyz, Specular}, {Emissive.xyz, IOR} (32 B/sphere)
 // r*r is precomputed on the host with the same f32 multiply the reference
 // repeats per test (main.cpp:406), so it is bit-identical.
@@ -27,6 +29,7 @@ struct TraceArgs {
     uint32_t n_groups, n_spheres, use_sky, flags;  // n_spheres: scalar rule set only
     uint32_t band_rows, band_count, band_index;
     uint32_t sec_threshold;      // lanes that must wait for a secondary iteration
+    uint32_t prefilter;          // secondary sphere loop: FMA prefilter + exact recheck (r2p valid)
     unsigned long long *stats;   // optional (RT_STATS): kStat* counters, NULL = off
     unsigned long long *wave_times;  // optional (RT_WAVETIMES): per-wave {start, end} s_memrealtime
 };
@@ -36,9 +39,9 @@ enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriG
 
 // Dynamic LDS per block: rsqrt table + fold table + groups + materials.
 static inline size_t rtk_lds_bytes(uint32_t n_groups) {
-    return 8192u + 2048u + (size_t)n_groups * 64u + (size_t)n_groups * 128u;
+    return 8192u + 2048u + (size_t)n_groups * (16u * kGroupF4) + (size_t)n_groups * 128u;
 }
-static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / 192u;  // 288 groups = 1152 spheres
+static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4 + 128u);  // 265 groups
 
 extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
                                 hipStream_t stream);

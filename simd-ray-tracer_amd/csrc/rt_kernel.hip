@@ -28,6 +28,7 @@ namespace rtk {
 
 constexpr float kEps = 1e-4f;   // base.h:889 F32Epsilon
 constexpr float kFMax = 1e30f;  // base.h:891 F32Max
+constexpr float kPfDirTol = 1.0f / 65536.0f;  // |1 - |D|^2| bound of the secondary prefilter (host: rt_host.cpp)
 // RandomFloat's (Max-Min)/(f64)(u32)-1 rounded to f32 (base.h:985), for the
 // three ranges the path uses: (-0.5,0.5) and (0,1) -> 1, (-1,1) -> 2.
 constexpr float kInvRange1 = (float)(1.0 / 4294967295.0);
@@ -210,33 +211,38 @@ __device__ __forceinline__ void shade(const float *lut, float4 col_spec, float4 
 
 struct Group {
     float x[4], y[4], z[4], r2[4];
+    float r2p[4];  // prefilter threshold r^2 + E (see pair_prefilter)
 };
 
 template <int SRC>
 __device__ __forceinline__ Group load_group(const TraceArgs &a, const float4 *lds_groups, uint32_t g) {
     Group G;
-    float4 v0, v1, v2, v3;
+    float4 v0, v1, v2, v3, v4;
     if (SRC == kSrcLds) {
-        v0 = lds_groups[4 * g + 0];
-        v1 = lds_groups[4 * g + 1];
-        v2 = lds_groups[4 * g + 2];
-        v3 = lds_groups[4 * g + 3];
+        v0 = lds_groups[kGroupF4 * g + 0];
+        v1 = lds_groups[kGroupF4 * g + 1];
+        v2 = lds_groups[kGroupF4 * g + 2];
+        v3 = lds_groups[kGroupF4 * g + 3];
+        v4 = lds_groups[kGroupF4 * g + 4];
     } else {
         // constant address space: read-only for the kernel's lifetime, so a
         // wave-uniform index always becomes an s_load into SGPRs
         typedef float v4f __attribute__((ext_vector_type(4)));
         typedef const __attribute__((address_space(4))) v4f cv4f;
         cv4f *cg = (cv4f *)a.groups;
-        const v4f w0 = cg[4 * g + 0], w1 = cg[4 * g + 1], w2 = cg[4 * g + 2], w3 = cg[4 * g + 3];
+        const v4f w0 = cg[kGroupF4 * g + 0], w1 = cg[kGroupF4 * g + 1], w2 = cg[kGroupF4 * g + 2],
+                  w3 = cg[kGroupF4 * g + 3], w4 = cg[kGroupF4 * g + 4];
         v0 = make_float4(w0.x, w0.y, w0.z, w0.w);
         v1 = make_float4(w1.x, w1.y, w1.z, w1.w);
         v2 = make_float4(w2.x, w2.y, w2.z, w2.w);
         v3 = make_float4(w3.x, w3.y, w3.z, w3.w);
+        v4 = make_float4(w4.x, w4.y, w4.z, w4.w);
     }
     G.x[0] = v0.x; G.x[1] = v0.y; G.x[2] = v0.z; G.x[3] = v0.w;
     G.y[0] = v1.x; G.y[1] = v1.y; G.y[2] = v1.z; G.y[3] = v1.w;
     G.z[0] = v2.x; G.z[1] = v2.y; G.z[2] = v2.z; G.z[3] = v2.w;
     G.r2[0] = v3.x; G.r2[1] = v3.y; G.r2[2] = v3.z; G.r2[3] = v3.w;
+    G.r2p[0] = v4.x; G.r2p[1] = v4.y; G.r2p[2] = v4.z; G.r2p[3] = v4.w;
     return G;
 }
 
@@ -332,11 +338,117 @@ __device__ __forceinline__ f2 pair_dist(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 
     return d;
 }
 
+// Secondary-ray prefilter: an FMA estimate of |C - D*T|^2 for two spheres
+// in 10 packed ops instead of the exact test's 19:
+//   C = S - O ;  cc = |C|^2 ;  T = C.D ;  e = cc - T*T      (fused)
+// For |D|^2 within K = 2^-16 of 1 and every origin on a sphere of the scene
+// (true for all secondary rays: NextRayOrigin is a hit point), |e - dist|
+// where dist is the reference's exactly-rounded value (main.cpp:401-407) is
+// below E_j = M_j (32u + 1.01K), u = 2^-24, M_j a bound on |C|^2 for
+// sphere j over every such origin (derivation: DESIGN.md).  The host stores
+// r2p_j >= r^2_j + E_j (rounded up), so e >= r2p proves dist > r^2 -- the
+// sphere is missed under both rule sets -- and only groups where some lane
+// fails that proof run the exact test.  A wave with any lane outside the
+// |D|^2 bound runs the exact loop instead.
+__device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz) {
+    f2 cx, cy, cz, cc, T, e;
+    asm("v_pk_add_f32 %[cx], %[sx], %[rx] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[cy], %[sy], %[ry] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %[cz], %[sz], %[rz] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[cc], %[cz], %[cz]\n\t"
+        "v_pk_fma_f32 %[cc], %[cy], %[cy], %[cc]\n\t"
+        "v_pk_fma_f32 %[cc], %[cx], %[cx], %[cc]\n\t"
+        "v_pk_mul_f32 %[T], %[cx], %[rx] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_fma_f32 %[T], %[cy], %[ry], %[T] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[T], %[cz], %[rz], %[T] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[e], %[T], %[T], %[cc] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+        : [cx] "=&v"(cx), [cy] "=&v"(cy), [cz] "=&v"(cz), [cc] "=&v"(cc), [T] "=&v"(T), [e] "=&v"(e)
+        : [sx] "s"(sx), [sy] "s"(sy), [sz] "s"(sz), [rx] "v"(r.x), [ry] "v"(r.y), [rz] "v"(r.z));
+    return e;
+}
+
+// Group g for a secondary ray through the prefilter: one wave branch per
+// group; inside it the exact packed test (same ops as test_group) reruns for
+// both pairs and the exact candidate logic decides, so results are identical.
+template <bool SIMD>
+__device__ __forceinline__ void test_group_pf(const TraceArgs &a, const Group &G, uint32_t g, const RayPk &p, Hit &h) {
+    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
+    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
+    const bool f = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]) | !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
+    if (f) {
+        f2 T01, T23;
+        const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
+        const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
+        bool h0, h1, h2, h3;
+        if (SIMD) {
+            h0 = d01.x < G.r2[0];
+            h1 = d01.y < G.r2[1];
+            h2 = d23.x < G.r2[2];
+            h3 = d23.y < G.r2[3];
+        } else {
+            const uint32_t s0 = 4u * g;
+            h0 = s0 + 0u < a.n_spheres && !(d01.x > G.r2[0]);
+            h1 = s0 + 1u < a.n_spheres && !(d01.y > G.r2[1]);
+            h2 = s0 + 2u < a.n_spheres && !(d23.x > G.r2[2]);
+            h3 = s0 + 3u < a.n_spheres && !(d23.y > G.r2[3]);
+        }
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0]);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1]);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2]);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, G.r2[3]);
+    }
+}
+
+template <bool SIMD>
+__device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const RayPk &p, Hit &h,
+                                           uint32_t *hit_groups);
+
+// Group rows straight from the constant address space at a running pointer
+// (immediate offsets, no per-group address arithmetic).
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) v4f_t cv4f_t;
+__device__ __forceinline__ Group load_group_at(cv4f_t *cg) {
+    Group G;
+    const v4f_t w0 = cg[0], w1 = cg[1], w2 = cg[2], w3 = cg[3], w4 = cg[4];
+    G.x[0] = w0.x; G.x[1] = w0.y; G.x[2] = w0.z; G.x[3] = w0.w;
+    G.y[0] = w1.x; G.y[1] = w1.y; G.y[2] = w1.z; G.y[3] = w1.w;
+    G.z[0] = w2.x; G.z[1] = w2.y; G.z[2] = w2.z; G.z[3] = w2.w;
+    G.r2[0] = w3.x; G.r2[1] = w3.y; G.r2[2] = w3.z; G.r2[3] = w3.w;
+    G.r2p[0] = w4.x; G.r2p[1] = w4.y; G.r2p[2] = w4.z; G.r2p[3] = w4.w;
+    return G;
+}
+
+// The full sphere loop over all groups from SGPRs, two groups per trip with
+// ping-pong registers: group g+1 (then g+2) is in flight while g is tested.
+// The group array carries two padding groups, so both prefetches stay in
+// bounds.  PF: secondary rays through the prefilter; else the exact test.
+template <bool SIMD, bool PF>
+__device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const RayPk &ray, Hit &h, uint32_t *hit_groups) {
+    cv4f_t *gp = (cv4f_t *)a.groups;
+    Group A = load_group_at(gp);
+    uint32_t g = 0;
+    for (;;) {
+        const Group B = load_group_at(gp + kGroupF4);
+        if (PF) test_group_pf<SIMD>(a, A, g, ray, h);
+        else test_group<SIMD>(a, A, g, ray, h, hit_groups);
+        if (++g == a.n_groups) break;
+        // SMEM returns out of order (only lgkmcnt(0) orders them): make B
+        // resident before A's next load is issued, so testing B does not
+        // also wait for that load
+        asm volatile("" ::"s"(B.x[0]), "s"(B.r2p[0]) : "memory");
+        A = load_group_at(gp + 2 * kGroupF4);
+        gp += 2 * kGroupF4;
+        if (PF) test_group_pf<SIMD>(a, B, g, ray, h);
+        else test_group<SIMD>(a, B, g, ray, h, hit_groups);
+        if (++g == a.n_groups) break;
+    }
+}
+
 // All four spheres of group g; one wave-level branch per group, nested
 // branches only for the (rare) lanes that pass the distance test.
 template <bool SIMD>
 __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const RayPk &p, Hit &h,
-                                           uint32_t *hit_groups = nullptr) {
+                                           uint32_t *hit_groups) {
     f2 T01, T23;
     const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
     const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
@@ -461,15 +573,18 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
     __shared__ uint64_t s_mask[kWavesPerBlock][kMaxMaskWords];
-    __shared__ float4 s_ring[P > 1 ? kWavesPerBlock * NPIX * kRing : 1];
+    // ring slot s of pixel pl at s * kRingStride + pl: the 4 sample lanes of a
+    // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
+    constexpr uint32_t kRingStride = NPIX + 1u;
+    __shared__ float4 s_ring[P > 1 ? kWavesPerBlock * kRing * kRingStride : 1];
     const float *lut = reinterpret_cast<const float *>(smem);
     float2 *fold = reinterpret_cast<float2 *>(smem + 512);
     float4 *lds_groups = smem + 512 + kFoldTable / 2;
-    float4 *lds_mats = lds_groups + 4 * a.n_groups;
+    float4 *lds_mats = lds_groups + kGroupF4 * a.n_groups;
     {
         const float4 *glut = reinterpret_cast<const float4 *>(a.rsqrt_lut);
         for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) smem[i] = glut[i];
-        for (uint32_t i = threadIdx.x; i < 4u * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
+        for (uint32_t i = threadIdx.x; i < kGroupF4 * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
         for (uint32_t i = threadIdx.x; i < 8u * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
         // running-mean weights of frame k (main.cpp:484-487): 1/(p+1), p/(p+1)
         for (uint32_t i = threadIdx.x; i < kFoldTable; i += blockDim.x) {
@@ -477,7 +592,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
         }
         if (P > 1)
-            for (uint32_t i = threadIdx.x; i < kWavesPerBlock * NPIX * kRing; i += blockDim.x)
+            for (uint32_t i = threadIdx.x; i < kWavesPerBlock * kRing * kRingStride; i += blockDim.x)
                 s_ring[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 
@@ -491,7 +606,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     const bool valid = x < a.width && ly < a.local_rows;
     const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
     const bool owner = j == 0;
-    float4 *ring = s_ring + (wave * NPIX + pl) * kRing;
+    float4 *ring = s_ring + wave * kRing * kRingStride + pl;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     if (CULL) {
@@ -503,8 +618,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             const uint32_t g = w * 64u + lane;
             bool cand = false;
             if (g < a.n_groups) {
-                const float4 gx = a.groups[4 * g + 0], gy = a.groups[4 * g + 1], gz = a.groups[4 * g + 2],
-                             gr = a.groups[4 * g + 3];
+                const float4 gx = a.groups[kGroupF4 * g + 0], gy = a.groups[kGroupF4 * g + 1],
+                             gz = a.groups[kGroupF4 * g + 2], gr = a.groups[kGroupF4 * g + 3];
                 cand = cone_may_hit(a, c, gx.x, gy.x, gz.x, gr.x) || cone_may_hit(a, c, gx.y, gy.y, gz.y, gr.y) ||
                        cone_may_hit(a, c, gx.z, gy.z, gz.z, gr.z) || cone_may_hit(a, c, gx.w, gy.w, gz.w, gr.w);
             }
@@ -528,6 +643,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
     uint32_t nrays = 0;
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
+#ifdef RTK_DIAG_STAMPS
+    uint64_t st_cyc[6] = {0, 0, 0, 0, 0, 0};
+#endif
     Sample p;
     p.bounce = 0;
     p.cx = p.cy = p.cz = 0.0f;
@@ -541,6 +659,10 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         const uint64_t sec = __ballot(mode == 1u);
         const uint64_t alive = __ballot(mode != 2u || (owner && valid && folded < a.frames));
         if (alive == 0) break;
+#ifdef RTK_DIAG_STAMPS  // timing diagnostic: s_memtime per loop-trip phase (adds overhead)
+        uint64_t t_a = 0, t_b = 0;
+        bool t_sec = false;
+#endif
         if ((pri | sec) != 0) {
             // Secondary segments run the full sphere loop; let them gather until
             // enough lanes share one (or no primary work is ready).
@@ -549,6 +671,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
             }
+#ifdef RTK_DIAG_STAMPS
+            t_a = __builtin_amdgcn_s_memtime();
+            t_b = t_a;
+            t_sec = do_sec;
+#endif
             if (do_sec ? mode == 1u : can_start) {
                 if (!do_sec) start_sample(a, x, y, a.prev_count + k, p);
                 bool done;
@@ -568,20 +695,32 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                             while (m) {
                                 const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
                                 m &= m - 1;
-                                test_group<SIMD>(a, load_group<SRC>(a, lds_groups, g), g, ray, h);
+                                test_group<SIMD>(a, load_group<SRC>(a, lds_groups, g), g, ray, h, nullptr);
                             }
                         }
                     } else {
-                        // software-pipelined: group g+1's scalar load is in flight
-                        // while group g is tested (the group array carries one
-                        // padding group, so g+1 is always a valid address)
-                        Group next = load_group<SRC>(a, lds_groups, 0);
-                        for (uint32_t g = 0; g < a.n_groups; ++g) {
-                            const Group G = next;
-                            next = load_group<SRC>(a, lds_groups, g + 1u);
-                            test_group<SIMD>(a, G, g, ray, h, a.stats ? &st_sec_hit : nullptr);
+                        // Secondary rays: the prefiltered loop, whose error bound
+                        // needs |D|^2 within 2^-16 of 1 on every lane (else exact).
+                        const float u2 = __builtin_fmaf(p.rx.y, p.rx.y, __builtin_fmaf(p.ry.y, p.ry.y, p.rz.y * p.rz.y));
+                        const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
+                        if (SRC == kSrcSmem && pf) {
+                            all_groups_smem<SIMD, true>(a, ray, h, nullptr);
+                        } else if (SRC == kSrcSmem) {
+                            all_groups_smem<SIMD, false>(a, ray, h, a.stats ? &st_sec_hit : nullptr);
+                        } else {
+                            // software-pipelined: group g+1's load is in flight while
+                            // g is tested (the array carries padding groups)
+                            Group next = load_group<SRC>(a, lds_groups, 0);
+                            for (uint32_t g = 0; g < a.n_groups; ++g) {
+                                const Group G = next;
+                                next = load_group<SRC>(a, lds_groups, g + 1u);
+                                test_group<SIMD>(a, G, g, ray, h, a.stats ? &st_sec_hit : nullptr);
+                            }
                         }
                     }
+#ifdef RTK_DIAG_STAMPS
+                    t_b = __builtin_amdgcn_s_memtime();
+#endif
                     // ---- hit select (x64_math.h:579-585 HorizontalMin + first equal lane)
                     float tmin;
                     uint32_t sidx;
@@ -611,7 +750,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     } else {
                         // Re-derive the winner's HitNormal / NextRayOrigin exactly as
                         // they were formed at acceptance (main.cpp:423-429).
-                        const float *gsph = reinterpret_cast<const float *>(lds_groups) + 16u * (sidx >> 2) + (sidx & 3u);
+                        const float *gsph = reinterpret_cast<const float *>(lds_groups) + 4u * kGroupF4 * (sidx >> 2) + (sidx & 3u);
                         const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
                         const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
                         const float ipx = p.rx.y * tmin, ipy = p.ry.y * tmin, ipz = p.rz.y * tmin;
@@ -640,7 +779,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         accz = oz * inv + accz * ratio;
                         folded = k + 1u;
                     } else {
-                        ring[k % kRing] = make_float4(ox, oy, oz, 1.0f);  // ready
+                        ring[(k % kRing) * kRingStride] = make_float4(ox, oy, oz, 1.0f);  // ready
                     }
                     k += P;
                     mode = k < a.frames ? 0u : 2u;
@@ -649,13 +788,16 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 }
             }
         }
+#ifdef RTK_DIAG_STAMPS
+        const uint64_t t_c = __builtin_amdgcn_s_memtime();
+#endif
         if (P > 1 && owner && valid) {
             // ---- running-mean blend (main.cpp:484-489) of every finished sample, in order
             for (;;) {
                 if (folded >= a.frames) break;
-                const float4 r = ring[folded % kRing];
+                const float4 r = ring[(folded % kRing) * kRingStride];
                 if (r.w == 0.0f) break;
-                ring[folded % kRing].w = 0.0f;
+                ring[(folded % kRing) * kRingStride].w = 0.0f;
                 const uint32_t pc = a.prev_count + folded;
                 const float inv = folded < kFoldTable ? fold[folded].x : 1.0f / (float)(pc + 1u);
                 const float ratio = folded < kFoldTable ? fold[folded].y : (float)pc / (float)(pc + 1u);
@@ -665,6 +807,16 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 folded += 1u;
             }
         }
+#ifdef RTK_DIAG_STAMPS
+        if (t_a) {
+            const uint64_t t_d = __builtin_amdgcn_s_memtime();
+            const uint64_t tb = __builtin_amdgcn_readfirstlane((uint32_t)t_b) |
+                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t_b >> 32)) << 32);
+            st_cyc[t_sec ? 3 : 0] += tb - t_a;
+            st_cyc[t_sec ? 4 : 1] += t_c - tb;
+            st_cyc[t_sec ? 5 : 2] += t_d - t_c;
+        }
+#endif
     }
 
     if (valid && owner && a.frames > 0) {
@@ -691,6 +843,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatSecLanes, (unsigned long long)st_sec_lanes);
         atomicAdd(a.stats + kStatPriGroups, (unsigned long long)st_groups);
         atomicAdd(a.stats + kStatSecHitGroups, (unsigned long long)st_sec_hit);
+#ifdef RTK_DIAG_STAMPS
+        for (int i = 0; i < 6; ++i) atomicAdd(a.stats + kStatStamp + i, (unsigned long long)st_cyc[i]);
+#endif
     }
 }
 
