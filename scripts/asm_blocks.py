@@ -1,6 +1,6 @@
 """Basic-block instruction mix of one kernel in a hipcc -S listing.
 
-usage: python scripts/asm_blocks.py /tmp/k.s <kernel-symbol-substring> [min_instrs]
+usage: python scripts/asm_blocks.py /tmp/k.s <kernel-symbol-substring> [min_instrs] [label-to-dump]
 Prints, per block: label, line, VALU (of which packed / transcendental),
 SALU, branches, LDS, SMEM, and the loop comment hipcc attaches.
 """
@@ -9,6 +9,7 @@ import sys
 
 path, sym = sys.argv[1], sys.argv[2]
 min_n = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+dump = sys.argv[4] if len(sys.argv) > 4 else None
 text = open(path).read()
 start = None
 for m in re.finditer(r"^(\S+):\s*(;.*)?$", text, flags=re.M):
@@ -28,6 +29,7 @@ for i, l in enumerate(lines):
     if not s or s.startswith(";") or s.startswith("."):
         continue
     cur["ins"].append(s.split()[0])
+    cur.setdefault("text", []).append(s)
 blocks.append(cur)
 trans = ("v_sqrt", "v_rcp", "v_rsq", "v_exp", "v_log", "v_sin", "v_cos", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32")
 tot = {}
@@ -50,3 +52,7 @@ for b in blocks:
         print(f"{b['label']:>12s} L{b['line']:<5d} n={len(ins):4d} valu={c['valu']:3d} pk={c['pk']:3d} tr={c['trans']:2d} "
               f"salu={c['salu']:3d} br={c['br']:2d} lds={c['lds']:2d} smem={c['smem']:2d} nop={c['nop']:2d} wait={c['wait']:2d}  {b['note'][:60]}")
 print("TOTAL", tot)
+if dump:
+    for b in blocks:
+        if b["label"] == dump:
+            print("\n".join(b.get("text", [])))

@@ -160,15 +160,15 @@ static void put_material(float *dst, const rt_material &m) {
 static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd) {
     std::vector<uint32_t> hit;
     for (uint32_t s = 0; s < 4u * n_groups; ++s) {
-        const float r2 = gv[(s / 4u) * 4u * kGroupF4 + 12u + s % 4u];
+        const float r2 = gv[(s / 4u) * 4u * kGroupF4 + 4u * kRowR2 + s % 4u];
         if (simd ? r2 > 0.0f : r2 >= 0.0f) hit.push_back(s);
     }
     double ratio = 0.0;
     uint32_t n_ratio = 0;
     for (uint32_t j = 0; j < 4u * n_groups; ++j) {
         const uint32_t gj = (j / 4u) * 4u * kGroupF4, lj = j % 4u;
-        const float r2 = gv[gj + 12u + lj];
-        float &r2p = gv[gj + 16u + lj];
+        const float r2 = gv[gj + 4u * kRowR2 + lj];
+        float &r2p = gv[gj + 4u * kRowR2P + lj];
         if (!(simd ? r2 > 0.0f : r2 >= 0.0f) || !std::isfinite(r2)) {
             r2p = -INFINITY;
             continue;
@@ -176,9 +176,10 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
         double reach = 0.0;
         for (uint32_t i : hit) {
             const uint32_t gi = (i / 4u) * 4u * kGroupF4, li = i % 4u;
-            const double dx = (double)gv[gi + li] - gv[gj + lj], dy = (double)gv[gi + 4u + li] - gv[gj + 4u + lj],
-                         dz = (double)gv[gi + 8u + li] - gv[gj + 8u + lj];
-            const double ri = std::sqrt((double)gv[gi + 12u + li]);
+            const double dx = (double)gv[gi + 4u * kRowX + li] - gv[gj + 4u * kRowX + lj],
+                         dy = (double)gv[gi + 4u * kRowY + li] - gv[gj + 4u * kRowY + lj],
+                         dz = (double)gv[gi + 4u * kRowZ + li] - gv[gj + 4u * kRowZ + lj];
+            const double ri = std::sqrt((double)gv[gi + 4u * kRowR2 + li]);
             reach = std::max(reach, std::sqrt(dx * dx + dy * dy + dz * dz) + ri);
         }
         const double m = (reach * 1.001 + 1e-3) * (reach * 1.001 + 1e-3);
@@ -207,10 +208,10 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
         std::vector<float> gv((size_t)ng * 4 * kGroupF4), mv((size_t)ng * 32, 0.0f);
         for (uint32_t i = 0; i < ng; ++i) {
             for (int l = 0; l < 4; ++l) {
-                gv[i * 4 * kGroupF4 + 0 + l] = g[i].X[l];
-                gv[i * 4 * kGroupF4 + 4 + l] = g[i].Y[l];
-                gv[i * 4 * kGroupF4 + 8 + l] = g[i].Z[l];
-                gv[i * 4 * kGroupF4 + 12 + l] = g[i].Radii[l] * g[i].Radii[l];
+                gv[i * 4 * kGroupF4 + 4 * kRowX + l] = g[i].X[l];
+                gv[i * 4 * kGroupF4 + 4 * kRowY + l] = g[i].Y[l];
+                gv[i * 4 * kGroupF4 + 4 * kRowZ + l] = g[i].Z[l];
+                gv[i * 4 * kGroupF4 + 4 * kRowR2 + l] = g[i].Radii[l] * g[i].Radii[l];
                 const uint32_t s = 4u * i + (uint32_t)l;
                 if (s < scene->Materials.Count) put_material(&mv[(size_t)s * 8], m[s]);
             }
@@ -226,15 +227,15 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
         std::vector<float> gv((size_t)ngs * 4 * kGroupF4, 0.0f), mv((size_t)ngs * 32, 0.0f);
         for (uint32_t i = 0; i < ns; ++i) {
             const uint32_t gi = i / 4u, l = i % 4u;
-            gv[gi * 4 * kGroupF4 + 0 + l] = s[i].Position.x;
-            gv[gi * 4 * kGroupF4 + 4 + l] = s[i].Position.y;
-            gv[gi * 4 * kGroupF4 + 8 + l] = s[i].Position.z;
-            gv[gi * 4 * kGroupF4 + 12 + l] = s[i].Radius * s[i].Radius;
+            gv[gi * 4 * kGroupF4 + 4 * kRowX + l] = s[i].Position.x;
+            gv[gi * 4 * kGroupF4 + 4 * kRowY + l] = s[i].Position.y;
+            gv[gi * 4 * kGroupF4 + 4 * kRowZ + l] = s[i].Position.z;
+            gv[gi * 4 * kGroupF4 + 4 * kRowR2 + l] = s[i].Radius * s[i].Radius;
             put_material(&mv[(size_t)i * 8], s[i].Material);
         }
         // Padding lanes of the scalar packing are skipped by the kernel's
         // s < n_spheres test (the scalar loop runs to Count, main.cpp:547).
-        for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 4 * kGroupF4 + 12 + (i % 4u)] = -__builtin_inff();
+        for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 4 * kGroupF4 + 4 * kRowR2 + (i % 4u)] = -__builtin_inff();
         const bool pays = prefilter_rows(gv, ngs, false);
         d->prefilter[1] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
         int rc = upload_set(d, 1, gv, mv, ngs);
@@ -283,6 +284,10 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.film_h = cam->FilmH;
     a.width = desc->Width;
     a.height = desc->Height;
+    // f64 division then rounding to f32 is the correctly rounded f32 quotient
+    // (53 >= 2*24 + 2: double rounding is innocuous for division)
+    a.inv_width = (float)(1.0 / (double)(float)desc->Width);
+    a.inv_height = (float)(1.0 / (double)(float)desc->Height);
     a.local_rows = local_rows;
     a.prev_count = desc->PreviousRayCount;
     a.frames = desc->Frames;

@@ -6,11 +6,14 @@
 #include <stdint.h>
 
 enum { kSrcSmem = 0, kSrcLds = 1 };  // where the sphere loop reads its groups
-constexpr uint32_t kGroupF4 = 5;      // float4 rows per sphere group
+constexpr uint32_t kGroupF4 = 5;      // float4 rows per sphere group:
+constexpr uint32_t kRowX = 0, kRowY = 1, kRowZ = 2;  //   centres
+constexpr uint32_t kRowR2P = 3;       //   prefilter thresholds (rows 0-3 = one s_load_dwordx16)
+constexpr uint32_t kRowR2 = 4;        //   r*r
 enum { kFlagAccumZero = 1 };
 
 // HBM layout of an uploaded scene (per rule set):
-//   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r*r[4]}, {r2p[4]}  (80 B/group)
+//   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
 //               r2p = prefilter threshold of the secondary-ray sphere loop (rt_host.cpp)
 //   materials : 4*n_groups x 2 float4 = {Color.xyz, Specular}, {Emissive.xyz, IOR} (32 B/sphere)
 // r*r is precomputed on the host with the same f32 multiply the reference
@@ -24,6 +27,7 @@ struct TraceArgs {
     unsigned long long *rays;    // accumulated bounce segments
     float cam_pos[3], cam_x[3], cam_y[3], film_center[3];
     float film_w, film_h;
+    float inv_width, inv_height;  // RN(1/(f32)width), RN(1/(f32)height)
     uint32_t width, height, local_rows;
     uint32_t prev_count, frames, max_bounce;
     uint32_t n_groups, n_spheres, use_sky, flags;  // n_spheres: scalar rule set only

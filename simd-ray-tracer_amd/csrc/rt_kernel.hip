@@ -63,15 +63,56 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
     return (px + py) + pz;
 }
 
+// Short correctly rounded sequences (each checked against the compiler's
+// IEEE sequence by scripts/mathcheck.hip on gfx950: rcp_rn and sqrt_rn
+// exhaustively over every f32 in [2^-40, 2^40] / [2^-60, 2^60], div_rn on
+// 8.6e9 random and edge-case pairs; all bit-identical).
+// RN(1/b) for b in [2^-40, 2^40]: v_rcp_f32 (< 1 ulp) + one Newton step.
+__device__ __forceinline__ float rcp_rn(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+
+// RN(sqrt(x)) for x = 0 or x in [2^-60, 2^60]: v_sqrt_f32 (< 1 ulp) and
+// the +-1 ulp residual test (the compiler's sequence minus its
+// denormal/infinity range scaling).
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+    return r;
+}
+
+// RN(a/b) from y = RN(1/b) (Markstein: q0 = a*y, exact residual, one fma
+// correction) for b > 0 and a == +-0 or |a/b| >= 2^-100 (no underflow in
+// the residual); the sign bit of a is copied so -0/b stays -0.
+__device__ __forceinline__ float div_rn(float a, float b, float y) {
+    const float q0 = a * y;
+    const float q = __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
+    return __uint_as_float((__float_as_uint(q) & 0x7FFFFFFFu) | (__float_as_uint(a) & 0x80000000u));
+}
+
 // v3::Normalize (x64_math.h:234-245): IEEE divide by the correctly rounded
-// sqrt, zero when len^2 <= 1e-4.
+// sqrt, zero when len^2 <= 1e-4.  Fast path: one reciprocal shared by the
+// three quotients; lanes outside its proven range (a quotient below 2^-99
+// or len above 2^40) take the compiler's IEEE sequence.
 __device__ __forceinline__ void normalize(float &x, float &y, float &z) {
     const float l2 = dot3(x, y, z, x, y, z);
-    const float len = __builtin_sqrtf(l2);
     const bool keep = l2 > kEps;
-    x = keep ? x / len : 0.0f;
-    y = keep ? y / len : 0.0f;
-    z = keep ? z / len : 0.0f;
+    const float len = sqrt_rn(l2);
+    const float inv = rcp_rn(len);
+    float qx = div_rn(x, len, inv), qy = div_rn(y, len, inv), qz = div_rn(z, len, inv);
+    // (a zero component also takes the IEEE path: rare, and exact either way)
+    const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(qx), __builtin_fabsf(qy)), __builtin_fabsf(qz));
+    if (__builtin_expect(keep && (m < 0x1p-99f || len > 0x1p40f), 0)) {
+        qx = x / len;
+        qy = y / len;
+        qz = z / len;
+    }
+    x = keep ? qx : 0.0f;
+    y = keep ? qy : 0.0f;
+    z = keep ? qz : 0.0f;
 }
 
 // rsqrtss (x64_math.h:71-74) from the 2x1024 table: exponent parity + top
@@ -125,8 +166,10 @@ __device__ __forceinline__ void start_sample(const TraceArgs &a, uint32_t x, uin
     p.rng = seed_mix(((uint64_t)frame * a.height + y) * a.width + x);
     const float jx = rand_float(p.rng, -0.5f, kInvRange1);
     const float jy = rand_float(p.rng, -0.5f, kInvRange1);
-    const float fx = -1.0f + (((float)x + jx) * 2.0f) / (float)a.width;
-    const float fy = -1.0f + (((float)y + jy) * 2.0f) / (float)a.height;
+    // ((x + Jx) * 2) / W with W's reciprocal RN(1/W) from the host: the
+    // numerator is 0 or >= 2^-24, so div_rn's range condition holds
+    const float fx = -1.0f + div_rn(((float)x + jx) * 2.0f, (float)a.width, a.inv_width);
+    const float fy = -1.0f + div_rn(((float)y + jy) * 2.0f, (float)a.height, a.inv_height);
     const float kx = (fx * a.film_w) * 0.5f;
     const float ky = (fy * a.film_h) * 0.5f;
     const float px = (a.film_center[0] + kx * a.cam_x[0]) + ky * a.cam_y[0];
@@ -214,35 +257,32 @@ struct Group {
     float r2p[4];  // prefilter threshold r^2 + E (see pair_prefilter)
 };
 
+__device__ __forceinline__ void group_rows(Group &G, float4 x, float4 y, float4 z, float4 r2p, float4 r2) {
+    G.x[0] = x.x; G.x[1] = x.y; G.x[2] = x.z; G.x[3] = x.w;
+    G.y[0] = y.x; G.y[1] = y.y; G.y[2] = y.z; G.y[3] = y.w;
+    G.z[0] = z.x; G.z[1] = z.y; G.z[2] = z.z; G.z[3] = z.w;
+    G.r2p[0] = r2p.x; G.r2p[1] = r2p.y; G.r2p[2] = r2p.z; G.r2p[3] = r2p.w;
+    G.r2[0] = r2.x; G.r2[1] = r2.y; G.r2[2] = r2.z; G.r2[3] = r2.w;
+}
+
+// Group rows from the constant address space: read-only for the kernel's
+// lifetime, so a wave-uniform address always becomes s_loads into SGPRs
+// (immediate offsets from one base: rows 0-3 one dwordx16, row 4 a dwordx4).
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) v4f_t cv4f_t;
+__device__ __forceinline__ float4 f4(v4f_t v) { return make_float4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ Group load_group_at(cv4f_t *cg) {
+    Group G;
+    group_rows(G, f4(cg[kRowX]), f4(cg[kRowY]), f4(cg[kRowZ]), f4(cg[kRowR2P]), f4(cg[kRowR2]));
+    return G;
+}
+
 template <int SRC>
 __device__ __forceinline__ Group load_group(const TraceArgs &a, const float4 *lds_groups, uint32_t g) {
+    if (SRC == kSrcSmem) return load_group_at((cv4f_t *)a.groups + kGroupF4 * g);
     Group G;
-    float4 v0, v1, v2, v3, v4;
-    if (SRC == kSrcLds) {
-        v0 = lds_groups[kGroupF4 * g + 0];
-        v1 = lds_groups[kGroupF4 * g + 1];
-        v2 = lds_groups[kGroupF4 * g + 2];
-        v3 = lds_groups[kGroupF4 * g + 3];
-        v4 = lds_groups[kGroupF4 * g + 4];
-    } else {
-        // constant address space: read-only for the kernel's lifetime, so a
-        // wave-uniform index always becomes an s_load into SGPRs
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        typedef const __attribute__((address_space(4))) v4f cv4f;
-        cv4f *cg = (cv4f *)a.groups;
-        const v4f w0 = cg[kGroupF4 * g + 0], w1 = cg[kGroupF4 * g + 1], w2 = cg[kGroupF4 * g + 2],
-                  w3 = cg[kGroupF4 * g + 3], w4 = cg[kGroupF4 * g + 4];
-        v0 = make_float4(w0.x, w0.y, w0.z, w0.w);
-        v1 = make_float4(w1.x, w1.y, w1.z, w1.w);
-        v2 = make_float4(w2.x, w2.y, w2.z, w2.w);
-        v3 = make_float4(w3.x, w3.y, w3.z, w3.w);
-        v4 = make_float4(w4.x, w4.y, w4.z, w4.w);
-    }
-    G.x[0] = v0.x; G.x[1] = v0.y; G.x[2] = v0.z; G.x[3] = v0.w;
-    G.y[0] = v1.x; G.y[1] = v1.y; G.y[2] = v1.z; G.y[3] = v1.w;
-    G.z[0] = v2.x; G.z[1] = v2.y; G.z[2] = v2.z; G.z[3] = v2.w;
-    G.r2[0] = v3.x; G.r2[1] = v3.y; G.r2[2] = v3.z; G.r2[3] = v3.w;
-    G.r2p[0] = v4.x; G.r2p[1] = v4.y; G.r2p[2] = v4.z; G.r2p[3] = v4.w;
+    const float4 *r = lds_groups + kGroupF4 * g;
+    group_rows(G, r[kRowX], r[kRowY], r[kRowZ], r[kRowR2P], r[kRowR2]);
     return G;
 }
 
@@ -370,32 +410,36 @@ __device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz
 // Group g for a secondary ray through the prefilter: one wave branch per
 // group; inside it the exact packed test (same ops as test_group) reruns for
 // both pairs and the exact candidate logic decides, so results are identical.
+// The prefilter needs rows 0-3 only (SGPRs); r^2 of a flagged group comes
+// from the block's LDS copy.
 template <bool SIMD>
-__device__ __forceinline__ void test_group_pf(const TraceArgs &a, const Group &G, uint32_t g, const RayPk &p, Hit &h) {
+__device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
+                                              const RayPk &p, Hit &h) {
     const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
     const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
     const bool f = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]) | !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
     if (f) {
+        const float4 r2 = lds_groups[kGroupF4 * g + kRowR2];
         f2 T01, T23;
         const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
         const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
         bool h0, h1, h2, h3;
         if (SIMD) {
-            h0 = d01.x < G.r2[0];
-            h1 = d01.y < G.r2[1];
-            h2 = d23.x < G.r2[2];
-            h3 = d23.y < G.r2[3];
+            h0 = d01.x < r2.x;
+            h1 = d01.y < r2.y;
+            h2 = d23.x < r2.z;
+            h3 = d23.y < r2.w;
         } else {
             const uint32_t s0 = 4u * g;
-            h0 = s0 + 0u < a.n_spheres && !(d01.x > G.r2[0]);
-            h1 = s0 + 1u < a.n_spheres && !(d01.y > G.r2[1]);
-            h2 = s0 + 2u < a.n_spheres && !(d23.x > G.r2[2]);
-            h3 = s0 + 3u < a.n_spheres && !(d23.y > G.r2[3]);
+            h0 = s0 + 0u < a.n_spheres && !(d01.x > r2.x);
+            h1 = s0 + 1u < a.n_spheres && !(d01.y > r2.y);
+            h2 = s0 + 2u < a.n_spheres && !(d23.x > r2.z);
+            h3 = s0 + 3u < a.n_spheres && !(d23.y > r2.w);
         }
-        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0]);
-        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1]);
-        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2]);
-        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, G.r2[3]);
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w);
     }
 }
 
@@ -403,44 +447,27 @@ template <bool SIMD>
 __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, uint32_t g, const RayPk &p, Hit &h,
                                            uint32_t *hit_groups);
 
-// Group rows straight from the constant address space at a running pointer
-// (immediate offsets, no per-group address arithmetic).
-typedef float v4f_t __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(4))) v4f_t cv4f_t;
-__device__ __forceinline__ Group load_group_at(cv4f_t *cg) {
+// Rows 0-3 only (one s_load_dwordx16): what the prefilter reads.
+__device__ __forceinline__ Group load_group_pf_at(cv4f_t *cg) {
     Group G;
-    const v4f_t w0 = cg[0], w1 = cg[1], w2 = cg[2], w3 = cg[3], w4 = cg[4];
-    G.x[0] = w0.x; G.x[1] = w0.y; G.x[2] = w0.z; G.x[3] = w0.w;
-    G.y[0] = w1.x; G.y[1] = w1.y; G.y[2] = w1.z; G.y[3] = w1.w;
-    G.z[0] = w2.x; G.z[1] = w2.y; G.z[2] = w2.z; G.z[3] = w2.w;
-    G.r2[0] = w3.x; G.r2[1] = w3.y; G.r2[2] = w3.z; G.r2[3] = w3.w;
-    G.r2p[0] = w4.x; G.r2p[1] = w4.y; G.r2p[2] = w4.z; G.r2p[3] = w4.w;
+    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    group_rows(G, f4(cg[kRowX]), f4(cg[kRowY]), f4(cg[kRowZ]), f4(cg[kRowR2P]), z4);
     return G;
 }
 
-// The full sphere loop over all groups from SGPRs, two groups per trip with
-// ping-pong registers: group g+1 (then g+2) is in flight while g is tested.
-// The group array carries two padding groups, so both prefetches stay in
-// bounds.  PF: secondary rays through the prefilter; else the exact test.
+// The full sphere loop over all groups from SGPRs.  PF: secondary rays
+// through the prefilter; else the exact test.
 template <bool SIMD, bool PF>
-__device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const RayPk &ray, Hit &h, uint32_t *hit_groups) {
+__device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray, Hit &h,
+                                                uint32_t *hit_groups) {
     cv4f_t *gp = (cv4f_t *)a.groups;
-    Group A = load_group_at(gp);
-    uint32_t g = 0;
-    for (;;) {
-        const Group B = load_group_at(gp + kGroupF4);
-        if (PF) test_group_pf<SIMD>(a, A, g, ray, h);
-        else test_group<SIMD>(a, A, g, ray, h, hit_groups);
-        if (++g == a.n_groups) break;
-        // SMEM returns out of order (only lgkmcnt(0) orders them): make B
-        // resident before A's next load is issued, so testing B does not
-        // also wait for that load
-        asm volatile("" ::"s"(B.x[0]), "s"(B.r2p[0]) : "memory");
-        A = load_group_at(gp + 2 * kGroupF4);
-        gp += 2 * kGroupF4;
-        if (PF) test_group_pf<SIMD>(a, B, g, ray, h);
-        else test_group<SIMD>(a, B, g, ray, h, hit_groups);
-        if (++g == a.n_groups) break;
+    // one group in SGPRs at a time: its s_load (scalar-cache hit) is covered
+    // by the other waves on the SIMD -- measured as fast as a ping-pong
+    // prefetch, at half the SGPRs
+    for (uint32_t g = 0; g < a.n_groups; ++g, gp += kGroupF4) {
+        const Group G = PF ? load_group_pf_at(gp) : load_group_at(gp);
+        if (PF) test_group_pf<SIMD>(a, lds_groups, G, g, ray, h);
+        else test_group<SIMD>(a, G, g, ray, h, hit_groups);
     }
 }
 
@@ -618,8 +645,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             const uint32_t g = w * 64u + lane;
             bool cand = false;
             if (g < a.n_groups) {
-                const float4 gx = a.groups[kGroupF4 * g + 0], gy = a.groups[kGroupF4 * g + 1],
-                             gz = a.groups[kGroupF4 * g + 2], gr = a.groups[kGroupF4 * g + 3];
+                const float4 gx = a.groups[kGroupF4 * g + kRowX], gy = a.groups[kGroupF4 * g + kRowY],
+                             gz = a.groups[kGroupF4 * g + kRowZ], gr = a.groups[kGroupF4 * g + kRowR2];
                 cand = cone_may_hit(a, c, gx.x, gy.x, gz.x, gr.x) || cone_may_hit(a, c, gx.y, gy.y, gz.y, gr.y) ||
                        cone_may_hit(a, c, gx.z, gy.z, gz.z, gr.z) || cone_may_hit(a, c, gx.w, gy.w, gz.w, gr.w);
             }
@@ -704,9 +731,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         const float u2 = __builtin_fmaf(p.rx.y, p.rx.y, __builtin_fmaf(p.ry.y, p.ry.y, p.rz.y * p.rz.y));
                         const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
                         if (SRC == kSrcSmem && pf) {
-                            all_groups_smem<SIMD, true>(a, ray, h, nullptr);
+                            all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr);
                         } else if (SRC == kSrcSmem) {
-                            all_groups_smem<SIMD, false>(a, ray, h, a.stats ? &st_sec_hit : nullptr);
+                            all_groups_smem<SIMD, false>(a, lds_groups, ray, h, a.stats ? &st_sec_hit : nullptr);
                         } else {
                             // software-pipelined: group g+1's load is in flight while
                             // g is tested (the array carries padding groups)
