@@ -186,11 +186,12 @@ def main():
                 "work_per_launch": f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d, brute force)",
                 "note": "algorithmic ops count every sphere for every segment; the kernel culls sphere groups "
                         "for primary rays exactly, so it executes fewer ops and frac may exceed 1. The "
-                        "executed-instruction bound is 'issue' (PMC).",
+                        "executed-instruction view is 'issue' (PMC).",
                 "hbm": {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}}
         if pmc:
-            roof["issue"] = {k: round(pmc[k], 4) for k in ("valu_issue_frac", "valu_lane_utilisation") if k in pmc}
+            roof["issue"] = {k: round(pmc[k], 4) for k in ("valu_inst_per_simd_cycle", "valu_lane_utilisation") if k in pmc}
+            roof["issue"]["ceiling"] = "0.5 full-rate / 0.25 half-rate (v_pk_*, int mul) wave-instr per SIMD-cycle"
             roof["issue"]["source"] = pmc["file"]
             roof["traffic_source"] = pmc["file"] + " (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
         line = {

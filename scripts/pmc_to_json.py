@@ -31,10 +31,12 @@ if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     rec["hbm_bytes_per_dispatch"] = 2.0 * per["FETCH_SIZE"] * 1024 + per["WRITE_SIZE"] * 1024
 if "SQ_INSTS_VALU" in per and "GRBM_GUI_ACTIVE" in per:
     cycles = per["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
-    # a wave64 VALU instruction occupies its SIMD's issue port 4 cycles
-    # (16 f32 lanes/clk, packed pk_* ops included): 1024 SIMDs
+    # wave64 VALU instructions issued per SIMD per cycle (1024 SIMDs).  The
+    # ceiling is 0.5 for full-rate ops (f32 add/mul/fma, 32-bit logic: 2 cyc)
+    # and 0.25 for half-rate ones (v_pk_*_f32, integer mul/cvt/64-bit shifts,
+    # f64: 4 cyc); transcendentals 8 cyc (scripts/mb_ops.hip on gfx950)
     rec["gpu_cycles_per_dispatch"] = cycles
-    rec["valu_issue_frac"] = per["SQ_INSTS_VALU"] * 4.0 / (1024.0 * cycles)
+    rec["valu_inst_per_simd_cycle"] = per["SQ_INSTS_VALU"] / (1024.0 * cycles)
 if "SQ_THREAD_CYCLES_VALU" in per and "SQ_ACTIVE_INST_VALU" in per:
     rec["valu_lane_utilisation"] = per["SQ_THREAD_CYCLES_VALU"] / (64.0 * per["SQ_ACTIVE_INST_VALU"])
 json.dump(rec, open(out, "w"), indent=1, sort_keys=True)

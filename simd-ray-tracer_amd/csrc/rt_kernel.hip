@@ -680,7 +680,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     for (;;) {
         // ring space: sample k may start once k < folded + kRing (the oldest
         // unfolded sample's lane is never blocked, so this cannot deadlock)
-        const uint32_t folded_g = P > 1 ? (uint32_t)__shfl(folded, (int)(lane - j), 64) : folded;
+        // the pixel's owner lane (first of its P-lane quad slice) via DPP
+        const uint32_t folded_g =
+            P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
+            : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
+                     : folded;
         const bool can_start = mode == 0u && (P == 1 || k < folded_g + kRing);
         const uint64_t pri = __ballot(can_start);
         const uint64_t sec = __ballot(mode == 1u);
@@ -806,7 +810,13 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         accz = oz * inv + accz * ratio;
                         folded = k + 1u;
                     } else {
-                        ring[(k % kRing) * kRingStride] = make_float4(ox, oy, oz, 1.0f);  // ready
+                        // park Out*(1/n) and the ratio (n-1)/n of sample k's blend; the
+                        // sign bit of .w marks the slot ready (the ratio is >= 0)
+                        const uint32_t pc = a.prev_count + k;
+                        float2 w = fold[k < kFoldTable ? k : 0u];
+                        if (__builtin_expect(k >= kFoldTable, 0))
+                            w = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
+                        ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
                     k += P;
                     mode = k < a.frames ? 0u : 2u;
@@ -819,18 +829,23 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         const uint64_t t_c = __builtin_amdgcn_s_memtime();
 #endif
         if (P > 1 && owner && valid) {
-            // ---- running-mean blend (main.cpp:484-489) of every finished sample, in order
-            for (;;) {
-                if (folded >= a.frames) break;
-                const float4 r = ring[(folded % kRing) * kRingStride];
-                if (r.w == 0.0f) break;
+            // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
+            // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
+            // sample's lane; two ring slots are read at once
+            while (folded < a.frames) {
+                const float4 r0 = ring[(folded % kRing) * kRingStride];
+                const float4 r1 = ring[((folded + 1u) % kRing) * kRingStride];
+                if (!__builtin_signbit(r0.w)) break;
+                accx = r0.x + accx * -r0.w;
+                accy = r0.y + accy * -r0.w;
+                accz = r0.z + accz * -r0.w;
                 ring[(folded % kRing) * kRingStride].w = 0.0f;
-                const uint32_t pc = a.prev_count + folded;
-                const float inv = folded < kFoldTable ? fold[folded].x : 1.0f / (float)(pc + 1u);
-                const float ratio = folded < kFoldTable ? fold[folded].y : (float)pc / (float)(pc + 1u);
-                accx = r.x * inv + accx * ratio;
-                accy = r.y * inv + accy * ratio;
-                accz = r.z * inv + accz * ratio;
+                folded += 1u;
+                if (folded >= a.frames || !__builtin_signbit(r1.w)) break;
+                accx = r1.x + accx * -r1.w;
+                accy = r1.y + accy * -r1.w;
+                accz = r1.z + accz * -r1.w;
+                ring[(folded % kRing) * kRingStride].w = 0.0f;
                 folded += 1u;
             }
         }
