@@ -31,6 +31,7 @@ struct rt_device {
     uint32_t sec_threshold = 16;
     int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
+    uint32_t fast_sqrt[2] = {0, 0};  // per rule set: candidate sqrt in sqrt_rn's verified range
     int lanes_per_pixel = 4;
     unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
     unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
@@ -191,6 +192,18 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
     return n_ratio > 0 && ratio / n_ratio < 0.5;
 }
 
+// Whether every r^2 the exact test can accept is 0 or in [2^-36, 2^60]: then
+// a passing candidate's r^2 - dist is 0 or >= 2^-60 (it is >= ulp(r^2)/2 when
+// positive), the range where the kernel's short sqrt is verified exact.
+static uint32_t sqrt_range_ok(const std::vector<float> &gv, uint32_t n_groups, bool simd) {
+    for (uint32_t s = 0; s < 4u * n_groups; ++s) {
+        const float r2 = gv[(s / 4u) * 4u * kGroupF4 + 4u * kRowR2 + s % 4u];
+        if (!(simd ? r2 > 0.0f : r2 >= 0.0f)) continue;  // never accepted (padding)
+        if (r2 != 0.0f && !(r2 >= 0x1p-36f && r2 <= 0x1p60f)) return 0u;
+    }
+    return 1u;
+}
+
 extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
     const uint32_t ng = scene->SIMDSpheres.Count;
@@ -218,6 +231,7 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
         }
         const bool pays = prefilter_rows(gv, ng, true);
         d->prefilter[0] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
+        d->fast_sqrt[0] = sqrt_range_ok(gv, ng, true);
         int rc = upload_set(d, 0, gv, mv, ng);
         if (rc) return rc;
     }
@@ -238,6 +252,7 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
         for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 4 * kGroupF4 + 4 * kRowR2 + (i % 4u)] = -__builtin_inff();
         const bool pays = prefilter_rows(gv, ngs, false);
         d->prefilter[1] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
+        d->fast_sqrt[1] = sqrt_range_ok(gv, ngs, false);
         int rc = upload_set(d, 1, gv, mv, ngs);
         if (rc) return rc;
     }
@@ -301,6 +316,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.band_index = desc->BandIndex;
     a.sec_threshold = d->sec_threshold;
     a.prefilter = d->prefilter[rs];
+    a.fast_sqrt = d->fast_sqrt[rs];
     a.stats = d->d_stats;
     if (d->want_wave_times) {
         const size_t waves = (size_t)((desc->Width + 7u) / 8u) * ((local_rows + 7u) / 8u) * 4u * 4u;  // >= any shape

@@ -34,6 +34,7 @@ struct TraceArgs {
     uint32_t band_rows, band_count, band_index;
     uint32_t sec_threshold;      // lanes that must wait for a secondary iteration
     uint32_t prefilter;          // secondary sphere loop: FMA prefilter + exact recheck (r2p valid)
+    uint32_t fast_sqrt;          // every hittable r^2 is 0 or in [2^-36, 2^60] (candidate sqrt_rn)
     unsigned long long *stats;   // optional (RT_STATS): kStat* counters, NULL = off
     unsigned long long *wave_times;  // optional (RT_WAVETIMES): per-wave {start, end} s_memrealtime
 };

@@ -140,7 +140,7 @@ __device__ __forceinline__ uint32_t to_u8(float v) {  // main.cpp:341-343
 
 __device__ __forceinline__ float linear_to_srgb(float l) {  // main.cpp:312-329
     l = saturate(l);
-    return l < 0.0031308f ? l * 12.92f : __builtin_sqrtf(l);
+    return l < 0.0031308f ? l * 12.92f : sqrt_rn(l);  // l in [0.0031308, 1]
 }
 
 __device__ __forceinline__ float reflectance(float cos_t, float eta) {  // main.cpp:292-300
@@ -230,12 +230,13 @@ __device__ __forceinline__ void shade(const float *lut, float4 col_spec, float4 
         const float eta = inside ? ior : 1.0f / ior;
         const float dd = dot3(-p.rx.y, -p.ry.y, -p.rz.y, nx, ny, nz);
         const float cos_t = dd < 1.0f ? dd : 1.0f;  // _mm_min_ss
-        const float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        // 1 - c*c and |1 - q.q| are 0 or >= 2^-25 (or NaN): inside sqrt_rn's range
+        const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
         const bool cant = eta * sin_t > 1.0f;
         const float qx = eta * (p.rx.y + cos_t * nx);
         const float qy = eta * (p.ry.y + cos_t * ny);
         const float qz = eta * (p.rz.y + cos_t * nz);
-        const float q = -__builtin_sqrtf(__builtin_fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
+        const float q = -sqrt_rn(__builtin_fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
         float rx = qx + q * nx, ry = qy + q * ny, rz = qz + q * nz;
         normalize(rx, ry, rz);
         bool refl = cant;
@@ -311,13 +312,12 @@ __device__ __forceinline__ void hit_reset(Hit &h) {
 
 // Exact intersection of one candidate sphere (main.cpp:413-429 / 561-578),
 // given its T and |C - D*T|^2 from the packed distance test.
+// fast: the host proved every hittable r^2 is 0 or in [2^-36, 2^60], so
+// r^2 - dist (positive, hence >= ulp(r^2)/2, or exactly 0) is inside sqrt_rn's
+// verified range.
 template <bool SIMD, int L>
-__device__ __forceinline__ void candidate(Hit &h, uint32_t g, float T, float dist, float r2) {
-#ifdef RTK_DIAG_FAST_SQRT  // timing diagnostic only: 1-ulp hardware sqrt, not bit-exact
-    const float X = __builtin_amdgcn_sqrtf(r2 - dist);
-#else
-    const float X = __builtin_sqrtf(r2 - dist);
-#endif
+__device__ __forceinline__ void candidate(Hit &h, uint32_t g, float T, float dist, float r2, bool fast) {
+    const float X = fast ? sqrt_rn(r2 - dist) : __builtin_sqrtf(r2 - dist);
     float it = T - X;
     const bool in = it < kEps;
     if (in) it = T + X;
@@ -436,10 +436,10 @@ __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *
             h2 = s0 + 2u < a.n_spheres && !(d23.x > r2.z);
             h3 = s0 + 3u < a.n_spheres && !(d23.y > r2.w);
         }
-        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x);
-        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y);
-        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z);
-        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w);
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x, a.fast_sqrt != 0u);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y, a.fast_sqrt != 0u);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z, a.fast_sqrt != 0u);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w, a.fast_sqrt != 0u);
     }
 }
 
@@ -499,10 +499,10 @@ __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, u
 #else
     if (h0 | h1 | h2 | h3) {
 #endif
-        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0]);
-        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1]);
-        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2]);
-        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, G.r2[3]);
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0], a.fast_sqrt != 0u);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1], a.fast_sqrt != 0u);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2], a.fast_sqrt != 0u);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, G.r2[3], a.fast_sqrt != 0u);
     }
 }
 
