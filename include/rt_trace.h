@@ -224,6 +224,17 @@ int rt_debug_stats(rt_device *dev, uint64_t out[16], int reset);
  * the last trace launch, wave id = (blockIdx.y*gridDim.x + blockIdx.x)*4 + w.
  * Returns the number of waves copied (0 when disabled), < 0 on error. */
 int64_t rt_debug_wave_times(rt_device *dev, uint64_t *out, uint64_t max_waves);
+
+/* Host-side view of what rt_scene_upload derives for one rule set (no GPU
+ * needed): per sphere slot s = 4*group + lane, the r^2 the exact test uses
+ * and the secondary-ray prefilter threshold r2p (any ray whose
+ * origin lies on a scene sphere and |D|^2 is within 2^-16 of 1 that passes
+ * the exact test d < r^2 (d <= r^2 for the scalar rules) has prefilter
+ * estimate e < r2p).  *out_flags: bit 0 = prefilter enabled by default for
+ * this scene, bit 1 = candidate sqrt in the short sequence's range.
+ * Arrays may be NULL to query the count. */
+int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p, uint32_t capacity,
+                       uint32_t *out_count, uint32_t *out_flags);
 const char *rt_last_error(void);
 
 /* ----------------------------------------------- OnInit / OnRender driver */

@@ -110,6 +110,8 @@ SIGNATURES = {
     "rt_device_synchronize": (c_int, [c_void_p]),
     "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "rt_debug_wave_times": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
+    "rt_scene_prefilter": (c_int, [POINTER(RtScene), c_uint32, c_void_p, c_void_p, c_uint32, POINTER(c_uint32),
+                                   POINTER(c_uint32)]),
     "rt_last_error": (c_char_p, []),
     "rt_on_init": (c_int, [POINTER(RtInitParams)]),
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
@@ -219,6 +221,20 @@ def pixel_seed(x: int, y: int, frame: int, width: int, height: int) -> int:
 
 def band_local_rows(height: int, band_rows: int, band_count: int, band_index: int) -> int:
     return int(lib().rt_band_local_rows(height, band_rows, band_count, band_index))
+
+
+def scene_prefilter(scene: RtScene, simd: bool = True):
+    """(r2, r2p, flags) per sphere slot 4*group+lane as rt_scene_upload packs
+    them: the exact test's r^2, the secondary-ray prefilter threshold, and
+    flags bit 0 = prefilter on by default, bit 1 = short candidate sqrt."""
+    n, fl = c_uint32(), c_uint32()
+    _check(lib().rt_scene_prefilter(ctypes.byref(scene), int(simd), None, None, 0, ctypes.byref(n), ctypes.byref(fl)),
+           "rt_scene_prefilter")
+    r2 = np.zeros(n.value, np.float32)
+    r2p = np.zeros(n.value, np.float32)
+    _check(lib().rt_scene_prefilter(ctypes.byref(scene), int(simd), r2.ctypes.data, r2p.ctypes.data, n.value,
+                                    ctypes.byref(n), ctypes.byref(fl)), "rt_scene_prefilter")
+    return r2, r2p, int(fl.value)
 
 
 def rsqrt_table_builtin() -> np.ndarray:

@@ -204,21 +204,34 @@ static uint32_t sqrt_range_ok(const std::vector<float> &gv, uint32_t n_groups, b
     return 1u;
 }
 
-extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
-    if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
+// One rule set of a scene in the kernel's layout (see rt_kernel.h): rs 0 =
+// SIMD rules from SIMDSpheres (main.cpp:399-400) + Materials[4g+l]
+// (main.cpp:443-444); rs 1 = scalar rules from ScalarSpheres[s].Position/
+// Radius/Material (main.cpp:547-590), padding lanes r^2 = -inf (the kernel
+// also skips them by its s < n_spheres test: the scalar loop runs to Count).
+struct PackedSet {
+    std::vector<float> groups, mats;
+    uint32_t n_groups = 0;
+    bool prefilter_pays = false;
+    uint32_t fast_sqrt = 0;
+};
+
+static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
     const uint32_t ng = scene->SIMDSpheres.Count;
     const uint32_t ns = scene->ScalarSpheres.Count;
     if (ng == 0 || !scene->SIMDSpheres.Data || !scene->Materials.Data || ns == 0 || !scene->ScalarSpheres.Data)
-        return fail(RT_EINVAL, "rt_scene_upload: empty scene");
+        return fail(RT_EINVAL, "scene: empty scene");
     const uint32_t ngs = (ns + 3u) / 4u;
     if (ng > kMaxLdsGroups || ngs > kMaxLdsGroups)
-        return fail(RT_EINVAL, "rt_scene_upload: %u spheres exceed the LDS-staged limit of %u", ns, 4u * kMaxLdsGroups);
-    HIP_OK(hipSetDevice(d->ordinal));
-    // SIMD rules: SIMDSpheres (main.cpp:399-400) + Materials[4g+l] (main.cpp:443-444).
-    {
+        return fail(RT_EINVAL, "scene: %u spheres exceed the LDS-staged limit of %u", ns, 4u * kMaxLdsGroups);
+    const uint32_t n = rs == 0 ? ng : ngs;
+    p.n_groups = n;
+    p.groups.assign((size_t)n * 4 * kGroupF4, 0.0f);
+    p.mats.assign((size_t)n * 32, 0.0f);
+    std::vector<float> &gv = p.groups;
+    if (rs == 0) {
         const rt_sphere_group *g = (const rt_sphere_group *)scene->SIMDSpheres.Data;
         const rt_material *m = (const rt_material *)scene->Materials.Data;
-        std::vector<float> gv((size_t)ng * 4 * kGroupF4), mv((size_t)ng * 32, 0.0f);
         for (uint32_t i = 0; i < ng; ++i) {
             for (int l = 0; l < 4; ++l) {
                 gv[i * 4 * kGroupF4 + 4 * kRowX + l] = g[i].X[l];
@@ -226,40 +239,62 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
                 gv[i * 4 * kGroupF4 + 4 * kRowZ + l] = g[i].Z[l];
                 gv[i * 4 * kGroupF4 + 4 * kRowR2 + l] = g[i].Radii[l] * g[i].Radii[l];
                 const uint32_t s = 4u * i + (uint32_t)l;
-                if (s < scene->Materials.Count) put_material(&mv[(size_t)s * 8], m[s]);
+                if (s < scene->Materials.Count) put_material(&p.mats[(size_t)s * 8], m[s]);
             }
         }
-        const bool pays = prefilter_rows(gv, ng, true);
-        d->prefilter[0] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
-        d->fast_sqrt[0] = sqrt_range_ok(gv, ng, true);
-        int rc = upload_set(d, 0, gv, mv, ng);
-        if (rc) return rc;
-    }
-    // Scalar rules: ScalarSpheres[s].Position/Radius/Material (main.cpp:547-590).
-    {
+    } else {
         const rt_scalar_sphere *s = (const rt_scalar_sphere *)scene->ScalarSpheres.Data;
-        std::vector<float> gv((size_t)ngs * 4 * kGroupF4, 0.0f), mv((size_t)ngs * 32, 0.0f);
         for (uint32_t i = 0; i < ns; ++i) {
             const uint32_t gi = i / 4u, l = i % 4u;
             gv[gi * 4 * kGroupF4 + 4 * kRowX + l] = s[i].Position.x;
             gv[gi * 4 * kGroupF4 + 4 * kRowY + l] = s[i].Position.y;
             gv[gi * 4 * kGroupF4 + 4 * kRowZ + l] = s[i].Position.z;
             gv[gi * 4 * kGroupF4 + 4 * kRowR2 + l] = s[i].Radius * s[i].Radius;
-            put_material(&mv[(size_t)i * 8], s[i].Material);
+            put_material(&p.mats[(size_t)i * 8], s[i].Material);
         }
-        // Padding lanes of the scalar packing are skipped by the kernel's
-        // s < n_spheres test (the scalar loop runs to Count, main.cpp:547).
         for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 4 * kGroupF4 + 4 * kRowR2 + (i % 4u)] = -__builtin_inff();
-        const bool pays = prefilter_rows(gv, ngs, false);
-        d->prefilter[1] = d->prefilter_env < 0 ? (pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
-        d->fast_sqrt[1] = sqrt_range_ok(gv, ngs, false);
-        int rc = upload_set(d, 1, gv, mv, ngs);
+    }
+    p.prefilter_pays = prefilter_rows(gv, n, rs == 0);
+    p.fast_sqrt = sqrt_range_ok(gv, n, rs == 0);
+    return RT_OK;
+}
+
+extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
+    if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
+    PackedSet ps[2];
+    for (int rs = 0; rs < 2; ++rs) {
+        const int rc = pack_set(scene, rs, ps[rs]);
+        if (rc) return rc;
+    }
+    HIP_OK(hipSetDevice(d->ordinal));
+    for (int rs = 0; rs < 2; ++rs) {
+        d->prefilter[rs] = d->prefilter_env < 0 ? (ps[rs].prefilter_pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
+        d->fast_sqrt[rs] = ps[rs].fast_sqrt;
+        const int rc = upload_set(d, rs, ps[rs].groups, ps[rs].mats, ps[rs].n_groups);
         if (rc) return rc;
     }
     HIP_OK(hipStreamSynchronize(d->stream));
-    d->n_spheres = ns;
+    d->n_spheres = scene->ScalarSpheres.Count;
     d->use_sky = scene->UseSkyColor;
     d->scene_set = true;
+    return RT_OK;
+}
+
+extern "C" int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p,
+                                  uint32_t capacity, uint32_t *out_count, uint32_t *out_flags) {
+    if (!scene || !out_count) return fail(RT_EINVAL, "rt_scene_prefilter: NULL argument");
+    PackedSet p;
+    const int rc = pack_set(scene, enable_simd ? 0 : 1, p);
+    if (rc) return rc;
+    const uint32_t n = 4u * p.n_groups;
+    *out_count = n;
+    if (out_flags) *out_flags = (p.prefilter_pays ? 1u : 0u) | (p.fast_sqrt ? 2u : 0u);
+    if ((out_r2 || out_r2p) && capacity < n) return fail(RT_EINVAL, "rt_scene_prefilter: capacity %u < %u", capacity, n);
+    for (uint32_t s = 0; s < n; ++s) {
+        const size_t base = (size_t)(s / 4u) * 4u * kGroupF4 + s % 4u;
+        if (out_r2) out_r2[s] = p.groups[base + 4u * kRowR2];
+        if (out_r2p) out_r2p[s] = p.groups[base + 4u * kRowR2P];
+    }
     return RT_OK;
 }
 

@@ -196,3 +196,52 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
     assert np.array_equal(img.reshape(-1), ocur0)
     rt.on_render_wait()
     rt.on_shutdown()
+
+
+# Kernel variants selected at device creation (rt_host.cpp reads the env):
+# prefilter forced on/off, brute-force primaries, 1/2 lanes per pixel.  Every
+# variant must give the same bits as the oracle.
+VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CULL": "0"},
+                {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"}, {"RT_SEC_THRESHOLD": "1"}]
+
+
+@pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_kernel_variants_match_oracle(rt, orc, torch_cuda, monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    dev = rt.Device(0)
+    try:
+        for scene_idx, n, W, H, spp, B in [(1, 64, 64, 48, 6, 8), (0, None, 48, 32, 4, 5), (2, None, 40, 24, 2, 5)]:
+            for simd in (True, False):
+                s, o = _scenes(rt, orc, scene_idx, n)
+                cam = rt.camera_setup(s, W, H)
+                g = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=spp, bounces=B, simd=simd)
+                r = orc.render(o, orc.camera(o, W, H), W, H, frames=spp, max_bounce=B, simd=simd)
+                assert_same(*g, *r)
+    finally:
+        dev.close()
+
+
+def test_tiny_sphere_scene_takes_the_ieee_sqrt(rt, orc, torch_cuda, gdev):
+    """A sphere with r^2 below 2^-36 puts candidate square roots outside the
+    short sequence's verified range: the host must fall back (flag bit 1
+    clear) and the result stays exact."""
+    base = rt.scene_prefix(rt.scene_builtin(1), 16)
+    sp, _, _ = rt.scene_arrays(base)
+    sp = sp.copy()
+    sp[3, 4] = np.float32(2e-6)  # radius -> r^2 = 4e-12 < 2^-36
+    s = rt.scene_from_spheres(sp, look_at=(base.LookAt.x, base.LookAt.y, base.LookAt.z),
+                              distance=base.DefaultDistanceFromLookAt, x_angle=base.DefaultXAngle,
+                              y_height=base.DefaultYHeight)
+    for simd in (True, False):
+        assert not (rt.scene_prefilter(s, simd)[2] & 2)
+    _, groups, mats = rt.scene_arrays(s)
+    o = orc.Scene(sp, groups, mats, look_at=(base.LookAt.x, base.LookAt.y, base.LookAt.z),
+                  distance=base.DefaultDistanceFromLookAt, x_angle=base.DefaultXAngle,
+                  y_height=base.DefaultYHeight)
+    W, H = 64, 48
+    cam = rt.camera_setup(s, W, H)
+    for simd in (True, False):
+        g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=4, bounces=8, simd=simd)
+        r = orc.render(o, orc.camera(o, W, H), W, H, frames=4, max_bounce=8, simd=simd)
+        assert_same(*g, *r)

@@ -1,0 +1,113 @@
+"""CPU property test of the secondary-ray prefilter.
+
+The kernel skips a sphere for a secondary ray when the FMA estimate
+e = |C|^2 - (C.D)^2 satisfies e >= r2p, where r2p comes from the host
+(rt_scene_prefilter, the same code rt_scene_upload runs).  Skipping is only
+allowed if the reference-rounded exact test (main.cpp:401-409, restated op
+for op in numpy f32) rejects the sphere.  This checks that on rays the bound
+is meant for -- origins on scene spheres, |D|^2 within 2^-16 of 1 -- with
+random and near-tangent directions, under both rule sets.
+"""
+import numpy as np
+import pytest
+
+F = np.float32
+
+
+def fma(a, b, c):
+    # exact f32 product in f64, one rounding of the sum to f64, one to f32:
+    # within 1 ulp of a true fma -- far inside the bound's slack
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(F)
+
+
+def exact_dist(cx, cy, cz, dx, dy, dz):
+    """main.cpp:401-407 with every f32 op rounded separately."""
+    T = (cx * dx + cy * dy) + cz * dz
+    qx, qy, qz = cx - dx * T, cy - dy * T, cz - dz * T
+    return (qx * qx + qy * qy) + qz * qz
+
+
+def prefilter(cx, cy, cz, dx, dy, dz):
+    """rt_kernel.hip pair_prefilter, lane by lane."""
+    cc = fma(cx, cx, fma(cy, cy, cz * cz))
+    T = fma(cz, dz, fma(cy, dy, cx * dx))
+    return fma(-T, T, cc)
+
+
+def unit(v):
+    v = v.astype(F)
+    n = np.sqrt((v.astype(np.float64) ** 2).sum(-1, keepdims=True))
+    return (v / n).astype(F)
+
+
+def rays(rng, centres, radii, n):
+    """Origins on random scene spheres; half random directions, half aimed
+    at a random sphere's silhouette (d ~ r^2: the bound's tight case);
+    |D|^2 pushed up to 2^-17 away from 1."""
+    i = rng.integers(0, len(centres), n)
+    u = unit(rng.normal(size=(n, 3)))
+    o = (centres[i] + radii[i, None] * u).astype(F)
+    d = unit(rng.normal(size=(n, 3)))
+    half = n // 2
+    j = rng.integers(0, len(centres), half)
+    to = (centres[j] - o[:half]).astype(np.float64)
+    w = np.cross(to, rng.normal(size=(half, 3)))
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    tangent = to + w * radii[j, None] * (1.0 + rng.uniform(-2e-6, 2e-6, (half, 1)))
+    d[:half] = unit(tangent)
+    d = (d * F(1.0) + d * F(rng.uniform(-2**-18, 2**-18, (n, 1)))).astype(F)
+    u2 = (d.astype(np.float64) ** 2).sum(1)
+    assert np.all(np.abs(1.0 - u2) <= 2**-16)
+    return o, d
+
+
+@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 256), (0, None), (2, None)])
+@pytest.mark.parametrize("simd", [True, False])
+def test_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
+    scene = rt.scene_builtin(idx)
+    if n_spheres:
+        scene = rt.scene_prefix(scene, n_spheres)
+    r2, r2p, flags = rt.scene_prefilter(scene, simd)
+    sp, groups, _ = rt.scene_arrays(scene)
+    if simd:
+        cx_, cy_, cz_ = groups[:, 0:4].ravel(), groups[:, 4:8].ravel(), groups[:, 8:12].ravel()
+        radius = groups[:, 12:16].ravel()
+    else:
+        pad = (-len(sp)) % 4
+        cx_, cy_, cz_ = (np.concatenate([sp[:, k], np.zeros(pad, F)]) for k in range(3))
+        radius = np.concatenate([sp[:, 4], np.zeros(pad, F)])
+    centres = np.stack([cx_, cy_, cz_], 1).astype(F)
+    assert np.array_equal(r2[: len(radius)][r2 >= 0], (radius * radius)[r2 >= 0])
+    live = r2 > 0 if simd else r2 >= 0
+    rng = np.random.default_rng(7 + idx)
+    o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), 4000)
+    cx = centres[None, :, 0] - o[:, None, 0]
+    cy = centres[None, :, 1] - o[:, None, 1]
+    cz = centres[None, :, 2] - o[:, None, 2]
+    dx, dy, dz = d[:, None, 0], d[:, None, 1], d[:, None, 2]
+    dist = exact_dist(cx, cy, cz, dx, dy, dz)
+    e = prefilter(cx, cy, cz, dx, dy, dz)
+    hit = (dist < r2) if simd else ~(dist > r2)
+    hit &= live[None, :]
+    skipped = ~(e < r2p)
+    assert not np.any(hit & skipped), "prefilter skipped a sphere the exact test accepts"
+    assert hit.sum() > 0
+    if flags & 1:  # where it is enabled, the prefilter must actually cull
+        assert (~skipped).sum() < 1.5 * hit.sum() + 0.05 * hit.size
+
+
+def test_prefilter_rows_of_padding_are_never_flagged(rt):
+    s = rt.scene_prefix(rt.scene_builtin(1), 13)  # scalar packing pads 3 lanes
+    r2, r2p, _ = rt.scene_prefilter(s, simd=False)
+    assert len(r2) == 16 and np.all(np.isneginf(r2p[13:])) and np.all(np.isfinite(r2p[:13]))
+    assert np.all(r2p[:13] > r2[:13])
+
+
+def test_short_sqrt_flag_follows_the_radius_range(rt):
+    base = rt.scene_prefix(rt.scene_builtin(1), 16)
+    assert rt.scene_prefilter(base, True)[2] & 2 and rt.scene_prefilter(base, False)[2] & 2
+    sp, _, _ = rt.scene_arrays(base)
+    sp = sp.copy()
+    sp[3, 4] = np.float32(2e-6)  # r^2 = 4e-12 < 2^-36: outside the verified range
+    tiny = rt.scene_from_spheres(sp)
+    assert not rt.scene_prefilter(tiny, True)[2] & 2 and not rt.scene_prefilter(tiny, False)[2] & 2
