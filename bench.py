@@ -40,21 +40,36 @@ def ops_per_segment(n_spheres: int) -> int:
     return 21 * n_spheres + 70
 
 
+# BASELINE.json configs: C2 is the headline (1 GPU) and the
+# default; C4 is C2 on several GPUs; C3 / C5 are the large single- and
+# multi-GPU cases.  C1 is the CPU-only plumbing case (tests, not a bench line).
+CONFIGS = {
+    "c2": dict(width=1920, height=1080, spp=256, spheres=64, bounces=8),
+    "c3": dict(width=3840, height=2160, spp=1024, spheres=64, bounces=8),
+    "c5": dict(width=7680, height=4320, spp=4096, spheres=256, bounces=16),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--spp", type=int, default=256)
-    p.add_argument("--spheres", type=int, default=64)
-    p.add_argument("--bounces", type=int, default=8)
+    p.add_argument("--config", choices=sorted(CONFIGS), default="c2", help="BASELINE.json workload preset")
+    p.add_argument("--width", type=int)
+    p.add_argument("--height", type=int)
+    p.add_argument("--spp", type=int)
+    p.add_argument("--spheres", type=int)
+    p.add_argument("--bounces", type=int)
     p.add_argument("--scalar", action="store_true", help="RenderTileScalar rules instead of RenderTile")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--band-rows", type=int, default=8, help="rows per interleaved band (multiple of 8)")
-    return p.parse_args()
+    a = p.parse_args()
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def cpu_baseline(args, n_rays_gpu_step: int):
@@ -177,7 +192,9 @@ def main():
         achieved = ops / (kern_ms / 1e3) / 1e12
         fb_bytes = rows[0] * W * (16 + 4)  # accumulation + RGBA8 written once per launch
         hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
-        workload = f"C2: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
+        preset = all(getattr(args, k) == v for k, v in CONFIGS[args.config].items())
+        tag = args.config.upper() if preset else "custom"
+        workload = f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
         pmc = pmc_record(workload)
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
@@ -195,7 +212,7 @@ def main():
             roof["issue"]["source"] = pmc["file"]
             roof["traffic_source"] = pmc["file"] + " (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
         line = {
-            "metric": "Mrays/sec at 1920x1080, 256spp, 8 bounces, 64 spheres",
+            "metric": f"Mrays/sec at {W}x{H}, {S}spp, {B} bounces, {N} spheres",
             "value": round(value, 1),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -206,7 +223,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (first 64 spheres of the reference's Floating Spheres scene, default camera, "
+            "data": f"synthetic (first {N} spheres of the reference's Floating Spheres scene, default camera, "
                     "per-(pixel,frame) PCG seeds)",
             "config": {"workload": workload,
                        "width": W, "height": H, "spp": S, "spheres": N, "bounces": B,
