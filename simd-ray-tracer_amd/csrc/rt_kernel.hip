@@ -35,6 +35,11 @@ constexpr float kInvRange1 = (float)(1.0 / 4294967295.0);
 constexpr float kInvRange2 = (float)(2.0 / 4294967295.0);
 
 __device__ __forceinline__ uint32_t pcg(uint64_t &s) {  // base.h:954-963
+#ifdef RTK_DIAG_CHEAP_RNG  // timing diagnostic only: 32-bit LCG, wrong results
+    const uint32_t x = (uint32_t)s * 1664525u + 1013904223u;
+    s = x;
+    return x;
+#endif
     const uint64_t old = s;
     s = old * 6364136223846793005ULL + 1442695040888963407ULL;
     const uint32_t v = (uint32_t)(old >> 32) ^ (uint32_t)old;
@@ -47,6 +52,9 @@ __device__ __forceinline__ float rand_float(uint64_t &s, float lo, float inv) { 
 }
 
 __device__ __forceinline__ uint64_t seed_mix(uint64_t i) {  // main.cpp:668-675
+#ifdef RTK_DIAG_CHEAP_RNG
+    return (uint32_t)i * 0x9E3779B9u;
+#endif
     uint64_t s = 0x420247153476526ULL * i;
     s += 0x8442885C91A5C8DULL;
     s ^= s >> ((7u + i) % 64u);
@@ -417,6 +425,32 @@ __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *
                                               const RayPk &p, Hit &h) {
     const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
     const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
+#ifdef RTK_PF_PAIR_BRANCH  // A/B: one exact-recheck branch per sphere pair
+    const bool f01 = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]);
+    const bool f23 = !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
+    if (f01 | f23) {
+        const float4 r2 = lds_groups[kGroupF4 * g + kRowR2];
+        if (f01) {
+            f2 T01;
+            const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
+            const uint32_t s0 = 4u * g;
+            const bool h0 = SIMD ? d01.x < r2.x : s0 + 0u < a.n_spheres && !(d01.x > r2.x);
+            const bool h1 = SIMD ? d01.y < r2.y : s0 + 1u < a.n_spheres && !(d01.y > r2.y);
+            if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x, a.fast_sqrt != 0u);
+            if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y, a.fast_sqrt != 0u);
+        }
+        if (f23) {
+            f2 T23;
+            const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
+            const uint32_t s0 = 4u * g;
+            const bool h2 = SIMD ? d23.x < r2.z : s0 + 2u < a.n_spheres && !(d23.x > r2.z);
+            const bool h3 = SIMD ? d23.y < r2.w : s0 + 3u < a.n_spheres && !(d23.y > r2.w);
+            if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z, a.fast_sqrt != 0u);
+            if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w, a.fast_sqrt != 0u);
+        }
+    }
+    return;
+#endif
     const bool f = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]) | !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
     if (f) {
         const float4 r2 = lds_groups[kGroupF4 * g + kRowR2];
@@ -569,6 +603,15 @@ __device__ __forceinline__ bool cone_may_hit(const TraceArgs &a, const Cone &c, 
     return cos_phi >= cos_lim - 1e-4f;
 }
 
+// Scheduling counters (RT_STATS=1) are compiled in only with -DRTK_STATS
+// (the diagnostic build, `make variant NAME=stats KFLAGS=-DRTK_STATS`): the
+// production kernel carries no per-trip checks for them.
+#ifdef RTK_STATS
+constexpr bool kStats = true;
+#else
+constexpr bool kStats = false;
+#endif
+
 constexpr int kWavesPerBlock = 4;
 constexpr int kMaxMaskWords = (kMaxLdsGroups + 63) / 64;
 constexpr uint32_t kFoldTable = 256;
@@ -698,7 +741,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             // Secondary segments run the full sphere loop; let them gather until
             // enough lanes share one (or no primary work is ready).
             const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
-            if (a.stats) {
+            if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
             }
@@ -722,7 +765,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                             uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
                                          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32))
                                           << 32);
-                            if (a.stats) st_groups += __builtin_popcountll(m);
+                            if (kStats && a.stats) st_groups += __builtin_popcountll(m);
                             while (m) {
                                 const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
                                 m &= m - 1;
@@ -737,7 +780,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         if (SRC == kSrcSmem && pf) {
                             all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr);
                         } else if (SRC == kSrcSmem) {
-                            all_groups_smem<SIMD, false>(a, lds_groups, ray, h, a.stats ? &st_sec_hit : nullptr);
+                            all_groups_smem<SIMD, false>(a, lds_groups, ray, h, kStats && a.stats ? &st_sec_hit : nullptr);
                         } else {
                             // software-pipelined: group g+1's load is in flight while
                             // g is tested (the array carries padding groups)
@@ -745,7 +788,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                             for (uint32_t g = 0; g < a.n_groups; ++g) {
                                 const Group G = next;
                                 next = load_group<SRC>(a, lds_groups, g + 1u);
-                                test_group<SIMD>(a, G, g, ray, h, a.stats ? &st_sec_hit : nullptr);
+                                test_group<SIMD>(a, G, g, ray, h, kStats && a.stats ? &st_sec_hit : nullptr);
                             }
                         }
                     }
@@ -878,7 +921,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         a.wave_times[2 * wid + 0] = t_start;
         a.wave_times[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
     }
-    if (a.stats && lane == 0) {
+    if (kStats && a.stats && lane == 0) {
         atomicAdd(a.stats + kStatPriIters, (unsigned long long)st_pri_it);
         atomicAdd(a.stats + kStatPriLanes, (unsigned long long)st_pri_lanes);
         atomicAdd(a.stats + kStatSecIters, (unsigned long long)st_sec_it);
