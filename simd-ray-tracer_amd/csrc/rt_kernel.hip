@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t k = j;            // this lane's next (or current) sample
     uint32_t folded = 0;       // owner: samples folded so far
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
-    uint32_t nrays = 0;
+    uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
 #ifdef RTK_DIAG_STAMPS
     uint64_t st_cyc[6] = {0, 0, 0, 0, 0, 0};
@@ -725,13 +725,14 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             t_b = t_a;
             t_sec = do_sec;
 #endif
-            if (do_sec ? mode == 1u : can_start) {
+            const bool traces = do_sec ? mode == 1u : can_start;
+            if (a.max_bounce != 0) nrays += __builtin_popcountll(__ballot(traces));
+            if (traces) {
                 if (!do_sec) start_sample(a, x, y, a.prev_count + k, p);
                 bool done;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
                 } else {
-                    nrays += 1;
                     Hit h;
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
@@ -886,11 +887,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                      (to_u8(linear_to_srgb(accz)) << 16) | (255u << 24);
     }
 
-    // ---- ray counter (RaysCastInThread, main.cpp:390): wave sum, one atomic
-    uint32_t sum = nrays;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-    if (lane == 0 && sum) atomicAdd(a.rays, (unsigned long long)sum);
+    // ---- ray counter (RaysCastInThread, main.cpp:390): one atomic per wave
+    if (lane == 0 && nrays) atomicAdd(a.rays, (unsigned long long)nrays);
     if (a.wave_times && lane == 0) {
         const uint64_t wid = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4u + wave;
         a.wave_times[2 * wid + 0] = t_start;
