@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--band-rows", type=int, default=8, help="rows per interleaved band (multiple of 8)")
+    p.add_argument("--sim-ranks", type=int, default=0,
+                   help="diagnostic (1 GPU): trace only band residue 0 of this many ranks, i.e. one rank's share "
+                        "of a multi-GPU frame; prints that rank's kernel time, not a bench line")
     a = p.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
@@ -135,7 +138,8 @@ def main():
     dev = rt.Device(local)
     dev.upload_scene(scene)
     band_rows = args.band_rows
-    rows = [rt.band_local_rows(H, band_rows, world, r) for r in range(world)]
+    bands = args.sim_ranks if (world == 1 and args.sim_ranks > 1) else world
+    rows = [rt.band_local_rows(H, band_rows, bands, r) for r in range(bands)]
     maxr = max(rows)
     cur = torch.zeros(maxr * W, dtype=torch.int32, device="cuda")
     prev = torch.zeros((maxr * W, 4), dtype=torch.float32, device="cuda")
@@ -152,7 +156,7 @@ def main():
         if i is not None:
             ev[i][0].record(stream)
         dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
-                  prev_count=0, frames=S, max_bounce=B, simd=not args.scalar, band_rows=band_rows, band_count=world,
+                  prev_count=0, frames=S, max_bounce=B, simd=not args.scalar, band_rows=band_rows, band_count=bands,
                   band_index=rank, accum_zero=True, stream=stream.cuda_stream)
         if i is not None:
             ev[i][1].record(stream)
@@ -186,6 +190,12 @@ def main():
     total_rays = int(rays_per_step.item()) * args.steps
     value = total_rays / elapsed / 1e6
 
+    if bands != world:
+        if rank == 0:
+            print(json.dumps({"sim_ranks": bands, "rank0_rows": rows[0], "rank0_kernel_ms": round(kern_ms, 3),
+                              "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}))
+        dev.close()
+        return
     if rank == 0:
         rays_local = int(rays.item())  # rank 0's rays per launch
         ops = rays_local * ops_per_segment(N)

@@ -32,7 +32,8 @@ struct rt_device {
     int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
     uint32_t fast_sqrt[2] = {0, 0};  // per rule set: candidate sqrt in sqrt_rn's verified range
-    int lanes_per_pixel = 4;
+    int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
+    uint32_t cu_count = 256;
     unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
     unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
     size_t wave_times_cap = 0;
@@ -71,6 +72,11 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
         delete d;
         return fail(RT_ENOMEM, "rt_device_create: stream/LUT allocation failed");
     }
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
+            d->cu_count = (uint32_t)prop.multiProcessorCount;
+    }
     const char *src = getenv("RT_SPHERE_SRC");
     if (src && strcmp(src, "lds") == 0) d->src = kSrcLds;
     const char *cull = getenv("RT_CULL");  // 0: brute-force primary rays too (A/B)
@@ -82,7 +88,10 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
-    if (lp) d->lanes_per_pixel = atoi(lp) == 1 ? 1 : atoi(lp) == 2 ? 2 : 4;
+    if (lp) {
+        const int v = atoi(lp);
+        d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
+    }
     const char *st = getenv("RT_STATS");
     if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatCount * sizeof(unsigned long long)) == hipSuccess)
         (void)hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long));
@@ -365,7 +374,19 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     }
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, d->lanes_per_pixel, s) != 0)
+    // Lanes per pixel: enough lanes in flight for ~12 waves per wave slot
+    // (8 waves x 4 SIMDs x CUs), so the slowest pixels' sample chains do not
+    // leave the tail of the launch on a few CUs -- smaller per-GPU frames
+    // (multi-GPU bands) get more lanes per pixel; never more than the frames.
+    int lpp = d->lanes_per_pixel;
+    if (lpp == 0) {
+        const uint64_t pixels = (uint64_t)desc->Width * local_rows;
+        const uint64_t target = (uint64_t)d->cu_count * 4u * 8u * 64u * 12u;
+        lpp = 4;
+        while (lpp < 16 && pixels * (uint64_t)lpp < target) lpp *= 2;
+        while (lpp > 1 && (uint32_t)lpp / 2u >= desc->Frames) lpp /= 2;
+    }
+    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, lpp, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return RT_OK;
 }

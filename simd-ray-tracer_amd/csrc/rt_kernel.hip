@@ -590,7 +590,12 @@ constexpr bool kStats = false;
 constexpr int kWavesPerBlock = 4;
 constexpr int kMaxMaskWords = (kMaxLdsGroups + 63) / 64;
 constexpr uint32_t kFoldTable = 256;
-constexpr uint32_t kRing = 8;  // per-pixel out-of-order sample slots (LDS)
+// Per-pixel out-of-order sample slots (LDS ring): at least P (every sample
+// lane holds one sample in flight) plus slack.
+template <int P>
+struct Ring {
+    static constexpr uint32_t N = P <= 4 ? 8u : 2u * (uint32_t)P;
+};
 
 #ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) of the production (SMEM) kernels;
 #define RTK_MIN_WAVES_PER_SIMD 6   // 6 waves = 80 VGPRs: measured best on C2 (w1 55.2k, w6 57.7k,
@@ -607,18 +612,20 @@ constexpr uint32_t kRing = 8;  // per-pixel out-of-order sample slots (LDS)
 // of the kernel's tail.  Tiles: P=1 8x8, P=2 8x4, P=4 4x4 pixels per wave.
 template <int P>
 struct Shape {
-    static constexpr uint32_t TW = P == 4 ? 4u : 8u;
-    static constexpr uint32_t TH = P == 1 ? 8u : 4u;
+    static constexpr uint32_t TW = P <= 2 ? 8u : P <= 8 ? 4u : 2u;
+    static constexpr uint32_t TH = P == 1 ? 8u : P <= 4 ? 4u : 2u;
+    static_assert(TW * TH * P == 64, "a wave is 64 lanes");
 };
 
 template <bool SIMD, int SRC, bool CULL, int P>
 __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) void trace_kernel(TraceArgs a) {
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
+    constexpr uint32_t kRing = Ring<P>::N;
     extern __shared__ float4 smem[];
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
     __shared__ uint64_t s_mask[kWavesPerBlock][kMaxMaskWords];
-    // ring slot s of pixel pl at s * kRingStride + pl: the 4 sample lanes of a
+    // ring slot s of pixel pl at s * kRingStride + pl: the sample lanes of a
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
     __shared__ float4 s_ring[P > 1 ? kWavesPerBlock * kRing * kRingStride : 1];
@@ -702,6 +709,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         const uint32_t folded_g =
             P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
             : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
+            : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
                      : folded;
         const bool can_start = mode == 0u && (P == 1 || k < folded_g + kRing);
         const uint64_t pri = __ballot(can_start);
@@ -954,9 +962,13 @@ static void launch_p(const TraceArgs *a, int simd, int src, int cull, hipStream_
 
 extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
                                 hipStream_t stream) {
-    if (lanes_per_pixel == 4) launch_p<4>(a, simd, src, cull, stream);
-    else if (lanes_per_pixel == 2) launch_p<2>(a, simd, src, cull, stream);
-    else launch_p<1>(a, simd, src, cull, stream);
+    switch (lanes_per_pixel) {
+        case 16: launch_p<16>(a, simd, src, cull, stream); break;
+        case 8: launch_p<8>(a, simd, src, cull, stream); break;
+        case 4: launch_p<4>(a, simd, src, cull, stream); break;
+        case 2: launch_p<2>(a, simd, src, cull, stream); break;
+        default: launch_p<1>(a, simd, src, cull, stream); break;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
