@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--band-rows", type=int, default=8, help="rows per interleaved band (multiple of 8)")
+    p.add_argument("--verify", action="store_true",
+                   help="after timing, rank 0 re-renders the whole frame alone and checks the gathered frame is "
+                        "bit-identical (adds 'verified' to the line)")
     p.add_argument("--sim-ranks", type=int, default=0,
                    help="diagnostic (1 GPU): trace only band residue 0 of this many ranks, i.e. one rank's share "
                         "of a multi-GPU frame; prints that rank's kernel time, not a bench line")
@@ -127,48 +130,74 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    # BENCH_BACKEND=gloo + BENCH_SHARE_GPU=1: rehearsal of the multi-rank
+    # path with every rank on cuda:0 (a 1-GPU box); the real runs use RCCL
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("BENCH_SHARE_GPU") == "1" else local
+    torch.cuda.set_device(gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
 
     W, H, S, B, N = args.width, args.height, args.spp, args.bounces, args.spheres
     scene = rt.scene_prefix(rt.scene_builtin(1), N)
     cam = rt.camera_setup(scene, W, H)
-    dev = rt.Device(local)
+    dev = rt.Device(gpu)
     dev.upload_scene(scene)
     band_rows = args.band_rows
     bands = args.sim_ranks if (world == 1 and args.sim_ranks > 1) else world
     rows = [rt.band_local_rows(H, band_rows, bands, r) for r in range(bands)]
     maxr = max(rows)
-    cur = torch.zeros(maxr * W, dtype=torch.int32, device="cuda")
+    # Two frame slots: frame i's band image is gathered to rank 0 (RCCL, async)
+    # while frame i+1 is traced; rank 0 assembles frame i before frame i+2
+    # reuses its slot.  The timed region ends only after the last frame is
+    # assembled on rank 0.
+    cur = [torch.zeros(maxr * W, dtype=torch.int32, device="cuda") for _ in range(2)]
     prev = torch.zeros((maxr * W, 4), dtype=torch.float32, device="cuda")
     rays = torch.zeros(1, dtype=torch.int64, device="cuda")
-    gathered = full = None
+    gbuf = full = None
     if world > 1 and rank == 0:
-        gathered = [torch.empty_like(cur) for _ in range(world)]
+        gdev = "cuda" if backend == "nccl" else "cpu"
+        gbuf = [torch.empty((world, maxr * W), dtype=torch.int32, device=gdev) for _ in range(2)]
         full = torch.empty(H * W, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    state = {"n": 0, "pending": None}
+
+    def finish():  # frame whose gather is in flight -> assembled on rank 0
+        if state["pending"] is None:
+            return
+        work, slot = state["pending"]
+        state["pending"] = None
+        work.wait()
+        if rank == 0:
+            src = gbuf[slot] if backend == "nccl" else gbuf[slot].to("cuda")
+            rt.assemble_bands(src.data_ptr(), maxr * W * 4, full.data_ptr(), W, H, 4, band_rows, world,
+                              stream=stream.cuda_stream)
 
     def step(i=None):
+        slot = state["n"] % 2
+        state["n"] += 1
         rays.zero_()
         if i is not None:
             ev[i][0].record(stream)
-        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
-                  prev_count=0, frames=S, max_bounce=B, simd=not args.scalar, band_rows=band_rows, band_count=bands,
-                  band_index=rank, accum_zero=True, stream=stream.cuda_stream)
+        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur[slot].data_ptr(),
+                  rays_ptr=rays.data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
+                  band_rows=band_rows, band_count=bands, band_index=rank, accum_zero=True, stream=stream.cuda_stream)
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:  # RCCL gather of the band images to rank 0 over xGMI, then assembly
-            dist.gather(cur, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                stacked = torch.cat(gathered)
-                rt.assemble_bands(stacked.data_ptr(), maxr * W * 4, full.data_ptr(), W, H, 4, band_rows, world,
-                                  stream=stream.cuda_stream)
+            send = cur[slot] if backend == "nccl" else cur[slot].cpu()
+            work = dist.gather(send, list(gbuf[slot].unbind(0)) if rank == 0 else None, dst=0, async_op=True)
+            finish()
+            state["pending"] = (work, slot)
 
     for _ in range(max(args.warmup, 1)):
         step()
+    finish()
     torch.cuda.synchronize()
     rays_per_step = torch.tensor([int(rays.item())], dtype=torch.int64, device="cuda")
     if world > 1:
@@ -178,10 +207,25 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    verified = None
+    if args.verify and bands == world:  # rank 0 renders the whole frame alone and compares
+        if rank == 0:
+            ref_cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+            ref_prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+            ref_rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            dev.trace(cam, width=W, height=H, prev_ptr=ref_prev.data_ptr(), cur_ptr=ref_cur.data_ptr(),
+                      rays_ptr=ref_rays.data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
+                      band_rows=band_rows, band_count=1, band_index=0, accum_zero=True, stream=stream.cuda_stream)
+            torch.cuda.synchronize()
+            got = full if world > 1 else cur[(state["n"] - 1) % 2]
+            verified = bool(torch.equal(got, ref_cur))
+        if world > 1:
+            dist.barrier()
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -245,6 +289,8 @@ def main():
         stats = dev.debug_stats()
         if stats:
             line["sched_stats"] = stats
+        if verified is not None:
+            line["verified"] = verified
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, total_rays)
         print(json.dumps(line), flush=True)
