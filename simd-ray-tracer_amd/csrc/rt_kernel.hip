@@ -702,6 +702,34 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     p.bounce = 0;
     p.cx = p.cy = p.cz = 0.0f;
 
+    // Empty tile: no sphere group passes the tile's (conservative) cone test,
+    // so every primary ray of every sample misses; without a sky term each
+    // sample's Out is exactly 0 (main.cpp:433-440), its one segment still
+    // counts (main.cpp:390), and its blend is Final = 0*(1/n) + Prev*((n-1)/n)
+    // = RN(Prev*((n-1)/n)) -- folded here without generating the rays.
+    bool empty_tile = CULL && !a.use_sky && a.max_bounce != 0;
+    if (CULL)
+        for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_mask[wave][w] == 0;
+    if (empty_tile) {
+        if (valid && owner) {
+            for (uint32_t q = 0; q < a.frames; ++q) {
+                float ratio;
+                if (q < kFoldTable) {
+                    ratio = fold[q].y;
+                } else {
+                    const uint32_t pc = a.prev_count + q;
+                    ratio = (float)pc / (float)(pc + 1u);
+                }
+                accx = 0.0f + accx * ratio;
+                accy = 0.0f + accy * ratio;
+                accz = 0.0f + accz * ratio;
+            }
+        }
+        nrays = (uint64_t)__builtin_popcountll(__ballot(valid && owner)) * a.frames;
+        folded = a.frames;
+        mode = 2u;
+    }
+
     for (;;) {
         // ring space: sample k may start once k < folded + kRing (the oldest
         // unfolded sample's lane is never blocked, so this cannot deadlock)
@@ -744,6 +772,10 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     Hit h;
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
+#ifdef RTK_DIAG_NO_PRI_ISECT  // timing diagnostic only: primaries skip intersection (all miss)
+                    if (!do_sec) {
+                    } else
+#endif
                     if (CULL && !do_sec) {
                         for (uint32_t w = 0; w < n_words; ++w) {
                             uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
