@@ -422,34 +422,50 @@ __device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz
 // exact recheck of both pairs per flagged group.)
 // The prefilter needs rows 0-3 only (SGPRs); r^2 of a flagged group comes
 // from the block's LDS copy.
+// The exact recheck of one group's flagged sphere pairs (f01, f23): only such
+// a pair reruns the exact packed test (same ops as test_group) and the exact
+// candidate logic decides, so results are identical.
+template <bool SIMD>
+__device__ __forceinline__ void recheck_pairs(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
+                                              const RayPk &p, Hit &h, bool f01, bool f23) {
+    const float4 r2 = lds_groups[kGroupF4 * g + kRowR2];
+    if (f01) {
+        f2 T01;
+        const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
+        const uint32_t s0 = 4u * g;
+        const bool h0 = SIMD ? d01.x < r2.x : s0 + 0u < a.n_spheres && !(d01.x > r2.x);
+        const bool h1 = SIMD ? d01.y < r2.y : s0 + 1u < a.n_spheres && !(d01.y > r2.y);
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x, a.fast_sqrt != 0u);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y, a.fast_sqrt != 0u);
+    }
+    if (f23) {
+        f2 T23;
+        const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
+        const uint32_t s0 = 4u * g;
+        const bool h2 = SIMD ? d23.x < r2.z : s0 + 2u < a.n_spheres && !(d23.x > r2.z);
+        const bool h3 = SIMD ? d23.y < r2.w : s0 + 3u < a.n_spheres && !(d23.y > r2.w);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z, a.fast_sqrt != 0u);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w, a.fast_sqrt != 0u);
+    }
+}
+
+// Prefilter flags of group G's two sphere pairs for this lane's ray.
+__device__ __forceinline__ void prefilter_group(const Group &G, const RayPk &p, bool &f01, bool &f23) {
+    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
+    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
+    f01 = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]);
+    f23 = !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
+}
+
+// Group g for a secondary ray through the prefilter: one wave branch per
+// group, and inside it one per flagged pair.  (Measured: +5.5 % on C2 over
+// one exact recheck of both pairs per flagged group.)
 template <bool SIMD>
 __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
                                               const RayPk &p, Hit &h) {
-    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
-    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
-    const bool f01 = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]);
-    const bool f23 = !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
-    if (f01 | f23) {
-        const float4 r2 = lds_groups[kGroupF4 * g + kRowR2];
-        if (f01) {
-            f2 T01;
-            const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
-            const uint32_t s0 = 4u * g;
-            const bool h0 = SIMD ? d01.x < r2.x : s0 + 0u < a.n_spheres && !(d01.x > r2.x);
-            const bool h1 = SIMD ? d01.y < r2.y : s0 + 1u < a.n_spheres && !(d01.y > r2.y);
-            if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x, a.fast_sqrt != 0u);
-            if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y, a.fast_sqrt != 0u);
-        }
-        if (f23) {
-            f2 T23;
-            const f2 d23 = pair_dist(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
-            const uint32_t s0 = 4u * g;
-            const bool h2 = SIMD ? d23.x < r2.z : s0 + 2u < a.n_spheres && !(d23.x > r2.z);
-            const bool h3 = SIMD ? d23.y < r2.w : s0 + 3u < a.n_spheres && !(d23.y > r2.w);
-            if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z, a.fast_sqrt != 0u);
-            if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w, a.fast_sqrt != 0u);
-        }
-    }
+    bool f01, f23;
+    prefilter_group(G, p, f01, f23);
+    if (f01 | f23) recheck_pairs<SIMD>(a, lds_groups, G, g, p, h, f01, f23);
 }
 
 template <bool SIMD>
@@ -472,7 +488,8 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
     cv4f_t *gp = (cv4f_t *)a.groups;
     // one group in SGPRs at a time: its s_load (scalar-cache hit) is covered
     // by the other waves on the SIMD -- measured as fast as a ping-pong
-    // prefetch, at half the SGPRs
+    // prefetch, at half the SGPRs (and two groups per trip under one branch
+    // measured 2 % slower)
     for (uint32_t g = 0; g < a.n_groups; ++g, gp += kGroupF4) {
         const Group G = PF ? load_group_pf_at(gp) : load_group_at(gp);
         if (PF) test_group_pf<SIMD>(a, lds_groups, G, g, ray, h);
