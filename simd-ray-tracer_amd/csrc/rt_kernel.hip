@@ -532,36 +532,40 @@ __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, u
     }
 }
 
-// Conservative per-wave culling for primary rays.  All primary rays of an
-// 8x8 tile start at CameraPosition and point into the tile's film rectangle
-// (+-0.5 px jitter), i.e. inside a cone (axis A, half-angle theta).  A
-// sphere can pass the exact test d < r^2 only if the LINE through the
-// camera along some cone direction comes within r of its centre, i.e. if the
-// angle between +-C and A is below theta + asin(r/|C|).  The test below uses
-// an angular margin of 2e-3 rad and r'^2 = r^2 + 1e-3|C|^2 + 1e-6, orders of
-// magnitude above the f32 rounding of the exact test, so a group it rejects
-// is one every lane's exact test would miss: skipping it changes nothing.
+// Conservative per-wave culling for primary rays.  All primary rays of a
+// tile start at CameraPosition and point into the tile's film rectangle
+// (+-0.5 px jitter), i.e. inside a cone (axis A, half-angle theta).  A sphere
+// can pass the exact test d < r^2 only if the LINE through the camera along
+// some cone direction comes within r of its centre, i.e. if the angle between
+// +-C and A is below theta + asin(r/|C|).  The cone and the test are computed
+// in f64, so their own rounding is negligible; the margins cover the f32 path
+// the kernel actually traces: each traced direction lies within ~1e-6 rad of
+// the ideal cone (film point and Normalize rounding; |jitter| <= 0.5 + 1e-7 px,
+// covered by the 0.501 px bound), and the reference-rounded distance is within
+// 13.3u|C|^2 of the exact one -- the test uses a 1e-5 rad
+// angular margin and r'^2 = r^2 (1 + 1e-5) + 1e-5 |C|^2, ten times both.  A
+// group it rejects is one every lane's exact test misses: skipping it changes
+// nothing.
 struct Cone {
-    float ax, ay, az;     // axis
-    float cos_t, sin_t;   // inflated half-angle
+    double ax, ay, az;     // axis
+    double cos_t, sin_t;   // inflated half-angle
 };
 
-__device__ __forceinline__ Cone tile_cone(const TraceArgs &a, float u0, float u1, float v0, float v1) {
-    const float fcx = a.film_center[0] - a.cam_pos[0];
-    const float fcy = a.film_center[1] - a.cam_pos[1];
-    const float fcz = a.film_center[2] - a.cam_pos[2];
-    const float aa[2] = {(-1.0f + (u0 * 2.0f) / (float)a.width) * a.film_w * 0.5f,
-                         (-1.0f + (u1 * 2.0f) / (float)a.width) * a.film_w * 0.5f};
-    const float bb[2] = {(-1.0f + (v0 * 2.0f) / (float)a.height) * a.film_h * 0.5f,
-                         (-1.0f + (v1 * 2.0f) / (float)a.height) * a.film_h * 0.5f};
-    float cx[4], cy[4], cz[4];
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+__device__ __forceinline__ Cone tile_cone(const TraceArgs &a, double u0, double u1, double v0, double v1) {
+    const double fcx = (double)a.film_center[0] - a.cam_pos[0];
+    const double fcy = (double)a.film_center[1] - a.cam_pos[1];
+    const double fcz = (double)a.film_center[2] - a.cam_pos[2];
+    const double aa[2] = {(-1.0 + (u0 * 2.0) / a.width) * a.film_w * 0.5, (-1.0 + (u1 * 2.0) / a.width) * a.film_w * 0.5};
+    const double bb[2] = {(-1.0 + (v0 * 2.0) / a.height) * a.film_h * 0.5,
+                          (-1.0 + (v1 * 2.0) / a.height) * a.film_h * 0.5};
+    double cx[4], cy[4], cz[4];
+    double sx = 0.0, sy = 0.0, sz = 0.0;
     for (int i = 0; i < 4; ++i) {
-        const float ka = aa[i & 1], kb = bb[i >> 1];
-        float x = fcx + ka * a.cam_x[0] + kb * a.cam_y[0];
-        float y = fcy + ka * a.cam_x[1] + kb * a.cam_y[1];
-        float z = fcz + ka * a.cam_x[2] + kb * a.cam_y[2];
-        const float inv = 1.0f / __builtin_sqrtf(x * x + y * y + z * z);
+        const double ka = aa[i & 1], kb = bb[i >> 1];
+        const double x = fcx + ka * a.cam_x[0] + kb * a.cam_y[0];
+        const double y = fcy + ka * a.cam_x[1] + kb * a.cam_y[1];
+        const double z = fcz + ka * a.cam_x[2] + kb * a.cam_y[2];
+        const double inv = 1.0 / __builtin_sqrt(x * x + y * y + z * z);
         cx[i] = x * inv;
         cy[i] = y * inv;
         cz[i] = z * inv;
@@ -570,14 +574,14 @@ __device__ __forceinline__ Cone tile_cone(const TraceArgs &a, float u0, float u1
         sz += cz[i];
     }
     Cone c;
-    const float inv = 1.0f / __builtin_sqrtf(sx * sx + sy * sy + sz * sz);
+    const double inv = 1.0 / __builtin_sqrt(sx * sx + sy * sy + sz * sz);
     c.ax = sx * inv;
     c.ay = sy * inv;
     c.az = sz * inv;
-    float ct = 1.0f;
-    for (int i = 0; i < 4; ++i) ct = fminf(ct, c.ax * cx[i] + c.ay * cy[i] + c.az * cz[i]);
-    const float st = __builtin_sqrtf(fmaxf(0.0f, 1.0f - ct * ct));
-    const float cd = 0.999998f, sd = 0.002f;  // cos/sin of the 2e-3 rad margin
+    double ct = 1.0;
+    for (int i = 0; i < 4; ++i) ct = fmin(ct, c.ax * cx[i] + c.ay * cy[i] + c.az * cz[i]);
+    const double st = __builtin_sqrt(fmax(0.0, 1.0 - ct * ct));
+    const double cd = 0.99999999995, sd = 1e-5;  // cos/sin of the 1e-5 rad margin
     c.cos_t = ct * cd - st * sd;
     c.sin_t = st * cd + ct * sd;
     return c;
@@ -585,14 +589,15 @@ __device__ __forceinline__ Cone tile_cone(const TraceArgs &a, float u0, float u1
 
 __device__ __forceinline__ bool cone_may_hit(const TraceArgs &a, const Cone &c, float px, float py, float pz, float r2) {
     if (!(r2 >= 0.0f)) return false;  // padding lanes of the scalar packing (-inf)
-    const float qx = px - a.cam_pos[0], qy = py - a.cam_pos[1], qz = pz - a.cam_pos[2];
-    const float c2 = qx * qx + qy * qy + qz * qz;
-    const float rr = r2 + 1e-3f * c2 + 1e-6f;
+    const double qx = (double)px - a.cam_pos[0], qy = (double)py - a.cam_pos[1], qz = (double)pz - a.cam_pos[2];
+    const double c2 = qx * qx + qy * qy + qz * qz;
+    const double rr = (double)r2 * (1.0 + 1e-5) + 1e-5 * c2;
     if (rr >= c2) return true;  // the camera is (nearly) inside: never cull
-    const float sb = __builtin_sqrtf(rr / c2), cb = __builtin_sqrtf(1.0f - rr / c2);
-    const float cos_lim = c.cos_t * cb - c.sin_t * sb;  // cos(theta + beta)
-    const float cos_phi = fabsf(c.ax * qx + c.ay * qy + c.az * qz) / __builtin_sqrtf(c2);
-    return cos_phi >= cos_lim - 1e-4f;
+    const double sb = __builtin_sqrt(rr / c2), cb = __builtin_sqrt(1.0 - rr / c2);
+    if (c.cos_t <= 0.0) return true;  // cone wider than 90 degrees: no culling
+    const double cos_lim = c.cos_t * cb - c.sin_t * sb;  // cos(theta + beta)
+    const double cos_phi = fabs(c.ax * qx + c.ay * qy + c.az * qz) / __builtin_sqrt(c2);
+    return cos_phi >= cos_lim - 1e-12;
 }
 
 // Scheduling counters (RT_STATS=1) are compiled in only with -DRTK_STATS
@@ -681,8 +686,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     if (CULL) {
         // the wave's tile; band_rows % 8 == 0 keeps its TH rows contiguous
         const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
-        const Cone c = tile_cone(a, (float)x0 - 0.501f, (float)(x0 + TW - 1u) + 0.501f, (float)y0 - 0.501f,
-                                 (float)(y0 + TH - 1u) + 0.501f);
+        const Cone c = tile_cone(a, (double)x0 - 0.501, (double)(x0 + TW - 1u) + 0.501, (double)y0 - 0.501,
+                                 (double)(y0 + TH - 1u) + 0.501);
         for (uint32_t w = 0; w < n_words; ++w) {
             const uint32_t g = w * 64u + lane;
             bool cand = false;

@@ -245,3 +245,28 @@ def test_tiny_sphere_scene_takes_the_ieee_sqrt(rt, orc, torch_cuda, gdev):
         g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=4, bounces=8, simd=simd)
         r = orc.render(o, orc.camera(o, W, H), W, H, frames=4, max_bounce=8, simd=simd)
         assert_same(*g, *r)
+
+
+@pytest.mark.parametrize("scene_idx,n", [(1, 64), (1, 256), (0, None)])
+def test_cone_culling_is_exact_at_full_resolution(rt, orc, torch_cuda, monkeypatch, scene_idx, n):
+    """Primary-ray cone culling (tight f64 cones, per 4x4 / 2x2 tile) and the
+    empty-tile fast path must not change a single bit at the BASELINE
+    resolution: the culled kernel against the brute-force one (RT_CULL=0),
+    full 1920x1080 frame, several lanes-per-pixel shapes."""
+    s, _ = _scenes(rt, orc, scene_idx, n)
+    W, H = 1920, 1080
+    cam = rt.camera_setup(s, W, H)
+    out = {}
+    for env in ({"RT_CULL": "0", "RT_LANES_PER_PIXEL": "4"}, {"RT_LANES_PER_PIXEL": "4"},
+                {"RT_LANES_PER_PIXEL": "16"}, {"RT_LANES_PER_PIXEL": "1"}):
+        monkeypatch.delenv("RT_CULL", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        dev = rt.Device(0)
+        try:
+            out[tuple(env.items())] = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=3, bounces=8)
+        finally:
+            dev.close()
+    ref = out[(("RT_CULL", "0"), ("RT_LANES_PER_PIXEL", "4"))]
+    for key, g in out.items():
+        assert torch_cuda.equal(g[0], ref[0]) and torch_cuda.equal(g[1], ref[1]) and g[2] == ref[2], key
