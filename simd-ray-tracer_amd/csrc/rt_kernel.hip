@@ -912,22 +912,25 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         if (P > 1 && owner && valid) {
             // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
             // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
-            // sample's lane; two ring slots are read at once
-            while (folded < a.frames) {
-                const float4 r0 = ring[(folded % kRing) * kRingStride];
-                const float4 r1 = ring[((folded + 1u) % kRing) * kRingStride];
-                if (!__builtin_signbit(r0.w)) break;
-                accx = r0.x + accx * -r0.w;
-                accy = r0.y + accy * -r0.w;
-                accz = r0.z + accz * -r0.w;
-                ring[(folded % kRing) * kRingStride].w = 0.0f;
-                folded += 1u;
-                if (folded >= a.frames || !__builtin_signbit(r1.w)) break;
-                accx = r1.x + accx * -r1.w;
-                accy = r1.y + accy * -r1.w;
-                accz = r1.z + accz * -r1.w;
-                ring[(folded % kRing) * kRingStride].w = 0.0f;
-                folded += 1u;
+            // sample's lane.  The fold is one sequential chain per pixel, so the owner
+            // reads kFoldBatch ring slots per LDS round trip (more for more lanes).
+            constexpr uint32_t kFoldBatch = P >= 8 ? 4u : 2u;
+            bool more = true;
+            while (more && folded < a.frames) {
+                float4 r[kFoldBatch];
+#pragma unroll
+                for (uint32_t i = 0; i < kFoldBatch; ++i) r[i] = ring[((folded + i) % kRing) * kRingStride];
+#pragma unroll
+                for (uint32_t i = 0; i < kFoldBatch; ++i) {
+                    more = more && folded < a.frames && __builtin_signbit(r[i].w);
+                    if (more) {
+                        accx = r[i].x + accx * -r[i].w;
+                        accy = r[i].y + accy * -r[i].w;
+                        accz = r[i].z + accz * -r[i].w;
+                        ring[(folded % kRing) * kRingStride].w = 0.0f;
+                        folded += 1u;
+                    }
+                }
             }
         }
 #ifdef RTK_DIAG_STAMPS
