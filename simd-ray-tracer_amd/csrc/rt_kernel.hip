@@ -688,17 +688,25 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
         const Cone c = tile_cone(a, (double)x0 - 0.501, (double)(x0 + TW - 1u) + 0.501, (double)y0 - 0.501,
                                  (double)(y0 + TH - 1u) + 0.501);
+        // one sphere per lane (64 per ballot), folded into one bit per group
+        const float *gf = reinterpret_cast<const float *>(a.groups);
         for (uint32_t w = 0; w < n_words; ++w) {
-            const uint32_t g = w * 64u + lane;
-            bool cand = false;
-            if (g < a.n_groups) {
-                const float4 gx = a.groups[kGroupF4 * g + kRowX], gy = a.groups[kGroupF4 * g + kRowY],
-                             gz = a.groups[kGroupF4 * g + kRowZ], gr = a.groups[kGroupF4 * g + kRowR2];
-                cand = cone_may_hit(a, c, gx.x, gy.x, gz.x, gr.x) || cone_may_hit(a, c, gx.y, gy.y, gz.y, gr.y) ||
-                       cone_may_hit(a, c, gx.z, gy.z, gz.z, gr.z) || cone_may_hit(a, c, gx.w, gy.w, gz.w, gr.w);
+            uint64_t gm = 0;
+            for (uint32_t q = 0; q < 4u && (w * 64u + q * 16u) < a.n_groups; ++q) {
+                const uint32_t sph = (w * 64u + q * 16u) * 4u + lane;  // sphere slot 4*g + l
+                bool cand = false;
+                if (sph < 4u * a.n_groups) {
+                    const float *row = gf + (size_t)(sph >> 2) * (4u * kGroupF4) + (sph & 3u);
+                    cand = cone_may_hit(a, c, row[4u * kRowX], row[4u * kRowY], row[4u * kRowZ], row[4u * kRowR2]);
+                }
+                uint64_t m = __ballot(cand);
+                m |= (m >> 1) | (m >> 2) | (m >> 3);  // bit 4i: some sphere of group 16q+i
+                uint64_t bits = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 16u; ++i) bits |= ((m >> (4u * i)) & 1u) << i;
+                gm |= bits << (16u * q);
             }
-            const uint64_t m = __ballot(cand);
-            if (lane == 0) s_mask[wave][w] = m;
+            if (lane == 0) s_mask[wave][w] = gm;
         }
     }
     __syncthreads();
