@@ -212,12 +212,14 @@ int rt_assemble_bands(const void *d_compact, uint64_t rank_stride_bytes, void *d
 
 int rt_device_synchronize(rt_device *dev);
 
-/* Scheduling counters accumulated over trace launches when the process runs
- * with RT_STATS=1: [0] primary wave-iterations, [1] primary lane-segments,
+/* Scheduling counters accumulated over trace launches when the library is the
+ * diagnostic build (`make -C simd-ray-tracer_amd variant NAME=stats
+ * KFLAGS=-DRTK_STATS`, loaded via RT_TRACE_LIB) and the process runs with
+ * RT_STATS=1: [0] primary wave-iterations, [1] primary lane-segments,
  * [2] secondary wave-iterations, [3] secondary lane-segments, [4] sphere
  * groups tested by primary iterations after culling, [5] secondary groups
- * where some lane passed the distance test, [8..13] diagnostic-build cycle
- * stamps.  Returns 1 when enabled, 0 when not (out zeroed), < 0 on error. */
+ * (exact loop) where some lane passed the distance test.  Returns 1 when
+ * enabled, 0 when not (out zeroed), < 0 on error. */
 int rt_debug_stats(rt_device *dev, uint64_t out[16], int reset);
 
 /* With RT_WAVETIMES=1: {start, end} s_memrealtime (100 MHz) of every wave of

@@ -281,8 +281,7 @@ class Device:
         _check(rc, "rt_debug_stats")
         if rc == 0:
             return None
-        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups", "_6", "_7",
-                "cyc_pri_isect", "cyc_pri_shade", "cyc_pri_fold", "cyc_sec_isect", "cyc_sec_shade", "cyc_sec_fold"]
+        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups"]
         return {k: int(v) for k, v in zip(keys, out) if not k.startswith("_")}
 
     def debug_wave_times(self, max_waves: int = 1 << 22):

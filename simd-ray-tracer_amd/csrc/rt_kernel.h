@@ -39,7 +39,6 @@ struct TraceArgs {
     unsigned long long *wave_times;  // optional (RT_WAVETIMES): per-wave {start, end} s_memrealtime
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
-       kStatStamp = 8,  // RTK_DIAG_STAMPS: cycles in {pri,sec} x {intersect, select+shade, fold}
        kStatCount = 16 };
 
 // Dynamic LDS per block: rsqrt table + fold table + groups + materials.

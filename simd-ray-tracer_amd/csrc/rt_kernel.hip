@@ -2,23 +2,27 @@
 //
 // Replaces the reference's tile callback RenderTile / RenderTileScalar
 // (main.cpp:348-495 / 497-640) and its lane-4 math layer (x64_math.h,
-// base.h:474-887).  One HIP thread owns one pixel of a compact per-GPU band
-// image and folds ALL of this launch's frames (samples) for that pixel in
-// order, keeping the running mean in registers; the reference's 4-wide SIMD
-// lanes become the four per-residue-class minima each thread carries.
+// base.h:474-887).  A wave owns a small pixel tile with P lanes per pixel;
+// each lane traces its pixel's samples k = j, j+P, ... and the pixel's owner
+// lane folds every finished sample into the running mean strictly in sample
+// order, so the result is bit-identical to one thread per pixel folding all
+// of this launch's frames.  The reference's 4-wide SIMD lanes become the four
+// per-residue-class minima each lane carries.
 //
 // Exactness: built with -ffp-contract=off (every op rounds separately, as the
 // reference's SSE lane ops do), IEEE f32 denormals, correctly rounded sqrt and
-// division; the one FMA the reference's -mfma build emits (Reflectance,
-// main.cpp:299) is an explicit fmaf; rsqrtss is reproduced by table.
+// division (short verified sequences where their range is guaranteed); the
+// one FMA the reference's -mfma build emits (Reflectance, main.cpp:299) is an
+// explicit fmaf; rsqrtss is reproduced by table.
 //
-// Work shape: a wave = one 8x8 pixel tile (coherent rays), a block = 16x16.
-// Paths are regenerated per lane (a lane whose sample ends starts its next
-// sample on the next loop trip) so the sphere loop never idles on lanes whose
-// path already terminated.  The sphere loop reads wave-uniform sphere groups
-// either through the scalar cache into SGPRs (SRC_SMEM) or from the
-// block's LDS copy (SRC_LDS); per-lane gathers (winning sphere, material,
-// rsqrt table) always hit the LDS copy.
+// Work shape: lanes alternate between starting primary rays
+// and gathering secondary segments; primary rays test only the sphere groups
+// their tile's cone can reach (tiles whose cone reaches none fold their
+// samples without tracing); secondary rays run an FMA prefilter with a proven
+// error bound and re-test exactly only the sphere pairs it flags.  Sphere
+// groups are wave-uniform: read through the scalar cache into SGPRs (SRC_SMEM)
+// or, for A/B, from the block's LDS copy (SRC_LDS); per-lane gathers (winning
+// sphere, material, r^2 of flagged groups, rsqrt table) hit the LDS copy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,11 +39,6 @@ constexpr float kInvRange1 = (float)(1.0 / 4294967295.0);
 constexpr float kInvRange2 = (float)(2.0 / 4294967295.0);
 
 __device__ __forceinline__ uint32_t pcg(uint64_t &s) {  // base.h:954-963
-#ifdef RTK_DIAG_CHEAP_RNG  // timing diagnostic only: 32-bit LCG, wrong results
-    const uint32_t x = (uint32_t)s * 1664525u + 1013904223u;
-    s = x;
-    return x;
-#endif
     const uint64_t old = s;
     s = old * 6364136223846793005ULL + 1442695040888963407ULL;
     const uint32_t v = (uint32_t)(old >> 32) ^ (uint32_t)old;
@@ -52,9 +51,6 @@ __device__ __forceinline__ float rand_float(uint64_t &s, float lo, float inv) { 
 }
 
 __device__ __forceinline__ uint64_t seed_mix(uint64_t i) {  // main.cpp:668-675
-#ifdef RTK_DIAG_CHEAP_RNG
-    return (uint32_t)i * 0x9E3779B9u;
-#endif
     uint64_t s = 0x420247153476526ULL * i;
     s += 0x8442885C91A5C8DULL;
     s ^= s >> ((7u + i) % 64u);
@@ -519,12 +515,7 @@ __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, u
         h3 = s0 + 3u < a.n_spheres && !(d23.y > G.r2[3]);
     }
     if (hit_groups && __ballot(h0 | h1 | h2 | h3)) *hit_groups += 1;
-#ifdef RTK_DIAG_NO_CANDIDATE  // timing diagnostic only: wrong results
-    h.ins |= (h0 | h1 | h2 | h3) ? 16u : 0u;
-    if (false) {
-#else
     if (h0 | h1 | h2 | h3) {
-#endif
         if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, G.r2[0], a.fast_sqrt != 0u);
         if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, G.r2[1], a.fast_sqrt != 0u);
         if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, G.r2[2], a.fast_sqrt != 0u);
@@ -725,9 +716,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
     uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
-#ifdef RTK_DIAG_STAMPS
-    uint64_t st_cyc[6] = {0, 0, 0, 0, 0, 0};
-#endif
     Sample p;
     p.bounce = 0;
     p.cx = p.cy = p.cz = 0.0f;
@@ -774,10 +762,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         const uint64_t sec = __ballot(mode == 1u);
         const uint64_t alive = __ballot(mode != 2u || (owner && valid && folded < a.frames));
         if (alive == 0) break;
-#ifdef RTK_DIAG_STAMPS  // timing diagnostic: s_memtime per loop-trip phase (adds overhead)
-        uint64_t t_a = 0, t_b = 0;
-        bool t_sec = false;
-#endif
         if ((pri | sec) != 0) {
             // Secondary segments run the full sphere loop; let them gather until
             // enough lanes share one (or no primary work is ready).
@@ -786,11 +770,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
             }
-#ifdef RTK_DIAG_STAMPS
-            t_a = __builtin_amdgcn_s_memtime();
-            t_b = t_a;
-            t_sec = do_sec;
-#endif
             const bool traces = do_sec ? mode == 1u : can_start;
             if (a.max_bounce != 0) nrays += __builtin_popcountll(__ballot(traces));
             if (traces) {
@@ -802,10 +781,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     Hit h;
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
-#ifdef RTK_DIAG_NO_PRI_ISECT  // timing diagnostic only: primaries skip intersection (all miss)
-                    if (!do_sec) {
-                    } else
-#endif
                     if (CULL && !do_sec) {
                         for (uint32_t w = 0; w < n_words; ++w) {
                             uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
@@ -838,9 +813,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                             }
                         }
                     }
-#ifdef RTK_DIAG_STAMPS
-                    t_b = __builtin_amdgcn_s_memtime();
-#endif
                     // ---- hit select (x64_math.h:579-585 HorizontalMin + first equal lane)
                     float tmin;
                     uint32_t sidx;
@@ -914,9 +886,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 }
             }
         }
-#ifdef RTK_DIAG_STAMPS
-        const uint64_t t_c = __builtin_amdgcn_s_memtime();
-#endif
         if (P > 1 && owner && valid) {
             // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
             // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
@@ -941,16 +910,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 }
             }
         }
-#ifdef RTK_DIAG_STAMPS
-        if (t_a) {
-            const uint64_t t_d = __builtin_amdgcn_s_memtime();
-            const uint64_t tb = __builtin_amdgcn_readfirstlane((uint32_t)t_b) |
-                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t_b >> 32)) << 32);
-            st_cyc[t_sec ? 3 : 0] += tb - t_a;
-            st_cyc[t_sec ? 4 : 1] += t_c - tb;
-            st_cyc[t_sec ? 5 : 2] += t_d - t_c;
-        }
-#endif
     }
 
     if (valid && owner && a.frames > 0) {
@@ -974,9 +933,6 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatSecLanes, (unsigned long long)st_sec_lanes);
         atomicAdd(a.stats + kStatPriGroups, (unsigned long long)st_groups);
         atomicAdd(a.stats + kStatSecHitGroups, (unsigned long long)st_sec_hit);
-#ifdef RTK_DIAG_STAMPS
-        for (int i = 0; i < 6; ++i) atomicAdd(a.stats + kStatStamp + i, (unsigned long long)st_cyc[i]);
-#endif
     }
 }
 
