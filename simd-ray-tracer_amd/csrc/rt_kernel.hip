@@ -729,7 +729,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     if (CULL)
         for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_mask[wave][w] == 0;
     if (empty_tile) {
-        if (valid && owner) {
+        // (an all-zero running mean stays exactly zero: nothing to fold)
+        if (valid && owner && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
             for (uint32_t q = 0; q < a.frames; ++q) {
                 float ratio;
                 if (q < kFoldTable) {
