@@ -11,5 +11,5 @@ for cfg in "${PCFG[@]}"; do
 done
 for cfg in "$@"; do
   env $cfg timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/b.json 2> gpurun_out/b.err || { tail -20 gpurun_out/b.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('gpurun_out/b.json')); print('$cfg', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d.get('sched_stats',''))"
+  python -c "import json,sys; d=json.load(open('gpurun_out/b.json')); print('$cfg', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['config']['rays_per_step'], d.get('sched_stats',''))"
 done

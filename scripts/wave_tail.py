@@ -1,4 +1,6 @@
-"""Diagnostic: per-wave start/end times of one C2 launch -> occupancy over time."""
+"""Diagnostic: per-wave start/end times of one C2 launch -> occupancy over time.
+env: SPP (256), SIM_RANKS (1: whole frame; G: rank 0's bands of a G-GPU split),
+RT_LANES_PER_PIXEL (auto)."""
 import os
 import sys
 import pathlib
@@ -13,12 +15,14 @@ scene = rt.scene_prefix(rt.scene_builtin(1), N)
 cam = rt.camera_setup(scene, W, H)
 dev = rt.Device(0)
 dev.upload_scene(scene)
-prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
-cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+G = int(os.environ.get("SIM_RANKS", "1"))
+rows = rt.band_local_rows(H, 8, G, 0)
+prev = torch.zeros((rows * W, 4), dtype=torch.float32, device="cuda")
+cur = torch.zeros(rows * W, dtype=torch.int32, device="cuda")
 rays = torch.zeros(1, dtype=torch.int64, device="cuda")
 for _ in range(2):
     dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
-              frames=S, max_bounce=B, accum_zero=True)
+              frames=S, max_bounce=B, accum_zero=True, band_rows=8, band_count=G, band_index=0)
 torch.cuda.synchronize()
 wt = dev.debug_wave_times().astype(np.int64)
 wt = wt[wt[:, 1] > 0]
@@ -28,11 +32,9 @@ dur = en - st
 print(f"waves {len(wt)}  kernel span {en.max():.0f} us  wave dur mean {dur.mean():.0f} p50 {np.median(dur):.0f} "
       f"p90 {np.percentile(dur, 90):.0f} max {dur.max():.0f} us")
 T = en.max()
+fin = np.sort(en)
+print("finished fraction -> time (us):", {q: round(float(fin[int(q * (len(fin) - 1))]), 0) for q in (0.5, 0.9, 0.99, 1.0)})
 for f in np.linspace(0, 1, 21)[:-1]:
     t = f * T
     print(f"t={t:8.0f}us active waves {int(((st <= t) & (en > t)).sum()):6d}")
-gx = (W + 7) // 8
-wid = np.arange(len(wt))
-bx, by, w = (wid // 4) % gx, (wid // 4) // gx, wid % 4
-slow = np.argsort(-dur)[:10]
-print("slowest waves (tile x,y):", [(int(bx[i] * 8 + (w[i] & 1) * 4), int(by[i] * 8 + (w[i] >> 1) * 4), int(dur[i])) for i in slow])
+print("slowest wave durations (us):", [int(d) for d in np.sort(dur)[-10:]])

@@ -33,6 +33,15 @@ struct rt_device {
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
     uint32_t fast_sqrt[2] = {0, 0};  // per rule set: candidate sqrt in sqrt_rn's verified range
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
+    // heaviest-first tile order learned from the previous launch of the same
+    // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
+    int tile_sched = 1;
+    uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_hist = nullptr;
+    size_t tile_cap = 0;
+    uint64_t tile_key = 0;
+    bool tile_order_valid = false;
+    hipStream_t tile_stream = nullptr;
+    bool tile_stream_set = false;
     uint32_t cu_count = 256;
     unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
     unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
@@ -85,6 +94,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (thr) d->sec_threshold = (uint32_t)atoi(thr);
     const char *pf = getenv("RT_PREFILTER");  // secondary-ray prefilter: 0 off, 1 on, unset = per-scene auto
     if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
+    const char *to = getenv("RT_TILE_ORDER");
+    if (to && to[0] == '0') d->tile_sched = 0;
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -110,6 +121,10 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_lut);
     (void)hipFree(d->d_stats);
     (void)hipFree(d->d_wave_times);
+    if (d->tile_stream_set) (void)hipStreamSynchronize(d->tile_stream);
+    (void)hipFree(d->d_tile_cost);
+    (void)hipFree(d->d_tile_order);
+    (void)hipFree(d->d_tile_hist);
     (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
@@ -374,20 +389,62 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     }
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-    // Lanes per pixel: enough lanes in flight for ~12 waves per wave slot
-    // (8 waves x 4 SIMDs x CUs), so the slowest pixels' sample chains do not
-    // leave the tail of the launch on a few CUs -- smaller per-GPU frames
-    // (multi-GPU bands) get more lanes per pixel; never more than the frames.
+    // Lanes per pixel (measured on MI355X at 1/2/4/8-way band splits of C2,
+    // bench.py --sim-ranks): 4 while the band has >= ~3k pixels per CU, else 8
+    // (more lanes per pixel shortens the per-lane sample chains that form the
+    // launch tail; 16 lost to 8 once tiles run heaviest-first); never more
+    // lanes than frames.
     int lpp = d->lanes_per_pixel;
     if (lpp == 0) {
         const uint64_t pixels = (uint64_t)desc->Width * local_rows;
-        const uint64_t target = (uint64_t)d->cu_count * 4u * 8u * 64u * 12u;
-        lpp = 4;
-        while (lpp < 16 && pixels * (uint64_t)lpp < target) lpp *= 2;
+        lpp = pixels >= (uint64_t)d->cu_count * 3072u ? 4 : 8;
         while (lpp > 1 && (uint32_t)lpp / 2u >= desc->Frames) lpp /= 2;
+    }
+    uint32_t n_tiles = 0;
+    // heaviest-first tile order: measured faster for 4 and 8 lanes per pixel,
+    // slower for 16 (identity order kept there)
+    const bool sched = d->tile_sched && lpp <= 8;
+    if (sched) {
+        // the order is a block -> tile map: only valid for the same launch
+        // geometry, and only once the sort that wrote it has run (same stream)
+        n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
+        const uint64_t key = ((uint64_t)desc->Width << 40) ^ ((uint64_t)local_rows << 20) ^ ((uint64_t)lpp << 14) ^
+                             ((uint64_t)band_rows << 8) ^ ((uint64_t)band_count << 4) ^ desc->BandIndex ^
+                             ((uint64_t)n_tiles << 32);
+        if (!d->tile_stream_set || s != d->tile_stream) {
+            if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(d->tile_stream));
+            d->tile_stream = s;
+            d->tile_stream_set = true;
+            d->tile_order_valid = false;
+        }
+        if (n_tiles > d->tile_cap) {
+            if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(s));
+            (void)hipFree(d->d_tile_cost);
+            (void)hipFree(d->d_tile_order);
+            (void)hipFree(d->d_tile_hist);
+            d->d_tile_cost = d->d_tile_order = d->d_tile_hist = nullptr;
+            if (hipMalloc(&d->d_tile_cost, n_tiles * 4u) != hipSuccess ||
+                hipMalloc(&d->d_tile_order, n_tiles * 4u) != hipSuccess ||
+                hipMalloc(&d->d_tile_hist, 64u * 4u) != hipSuccess)
+                return fail(RT_ENOMEM, "rt_trace: tile order buffers");
+            d->tile_cap = n_tiles;
+            d->tile_key = ~key;
+        }
+        if (key != d->tile_key) {
+            HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_tiles * 4u, s));
+            d->tile_key = key;
+            d->tile_order_valid = false;
+        }
+        a.tile_cost = d->d_tile_cost;
+        a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
     }
     if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, lpp, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (sched) {
+        if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_hist, n_tiles, s) != 0)
+            return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
+        d->tile_order_valid = true;
+    }
     return RT_OK;
 }
 

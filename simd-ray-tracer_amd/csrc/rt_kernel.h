@@ -37,6 +37,8 @@ struct TraceArgs {
     uint32_t fast_sqrt;          // every hittable r^2 is 0 or in [2^-36, 2^60] (candidate sqrt_rn)
     unsigned long long *stats;   // optional (RT_STATS): kStat* counters, NULL = off
     unsigned long long *wave_times;  // optional (RT_WAVETIMES): per-wave {start, end} s_memrealtime
+    const uint32_t *tile_order;  // optional: block -> tile map (heaviest first), NULL = identity
+    uint32_t *tile_cost;         // optional: per-tile cost (max wave shader cycles), atomicMax'd
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatCount = 16 };
@@ -49,5 +51,9 @@ static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4
 
 extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
                                 hipStream_t stream);
+// Heaviest-first tile order for the next launch from this launch's costs
+// (resets the costs); n = rtk_tile_count(...) of the launch geometry.
+extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *hist, uint32_t n, hipStream_t stream);
+extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lanes_per_pixel);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

@@ -663,8 +663,15 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
 
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint64_t t_start = a.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
-    const uint32_t x0 = blockIdx.x * (2u * TW) + (wave & 1u) * TW;
-    const uint32_t ly0 = blockIdx.y * (2u * TH) + (wave >> 1) * TH;
+    // Tile of this block: heaviest-first order from the previous launch's
+    // measured per-tile cost when the host supplies one (tile_order), so the
+    // long tiles do not start last and form the launch's tail.
+    const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t tile = a.tile_order ? a.tile_order[blk] : blk;
+    const uint32_t tile_x = tile % gridDim.x, tile_y = tile / gridDim.x;
+    const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t x0 = tile_x * (2u * TW) + (wave & 1u) * TW;
+    const uint32_t ly0 = tile_y * (2u * TH) + (wave >> 1) * TH;
     const uint32_t pl = lane / P, j = lane % P;  // pixel of the tile, sample lane of the pixel
     const uint32_t x = x0 + pl % TW;
     const uint32_t ly = ly0 + pl / TW;
@@ -922,8 +929,12 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
 
     // ---- ray counter (RaysCastInThread, main.cpp:390): one atomic per wave
     if (lane == 0 && nrays) atomicAdd(a.rays, (unsigned long long)nrays);
+    if (a.tile_cost && lane == 0) {
+        const uint64_t c = __builtin_amdgcn_s_memtime() - t_cost0;
+        atomicMax(a.tile_cost + tile, (uint32_t)(c < 0xFFFFFFFFull ? c : 0xFFFFFFFFull));
+    }
     if (a.wave_times && lane == 0) {
-        const uint64_t wid = ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4u + wave;
+        const uint64_t wid = (uint64_t)tile * 4u + wave;
         a.wave_times[2 * wid + 0] = t_start;
         a.wave_times[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -959,7 +970,59 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint8_t *src, uint6
     }
 }
 
+// ---- heaviest-first tile order for the next launch (counting sort of the
+// per-tile costs this launch measured into 32 log2 buckets, descending)
+__global__ __launch_bounds__(256) void tile_hist_kernel(const uint32_t *cost, uint32_t n, uint32_t *hist) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(hist + (31u - __builtin_clz(cost[i] | 1u)), 1u);
+}
+
+__global__ void tile_scan_kernel(uint32_t *hist) {  // hist[0..31] -> start offsets, heavy buckets first
+    if (threadIdx.x != 0) return;
+    uint32_t off = 0;
+    for (int b = 31; b >= 0; --b) {
+        const uint32_t c = hist[b];
+        hist[b] = off;
+        hist[32 + b] = 0;  // scatter cursor
+        off += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void tile_scatter_kernel(uint32_t *cost, uint32_t n, uint32_t *hist,
+                                                           uint32_t *order) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t b = 31u - __builtin_clz(cost[i] | 1u);
+    const uint32_t r = hist[b] + atomicAdd(hist + 32 + b, 1u);  // rank, heaviest first
+    // (consecutive blocks must stay of similar cost: blocks are dealt
+    // round-robin to the 8 XCDs, so alternating heavy and light tiles would
+    // put all heavy work on half of them -- measured 2x slower)
+    order[r] = i;
+    cost[i] = 0;  // measured afresh by the next launch
+}
+
 }  // namespace rtk
+
+extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *hist, uint32_t n, hipStream_t stream) {
+    (void)hipMemsetAsync(hist, 0, 64 * sizeof(uint32_t), stream);
+    const dim3 grid((n + 255u) / 256u);
+    hipLaunchKernelGGL(rtk::tile_hist_kernel, grid, dim3(256), 0, stream, (const uint32_t *)cost, n, hist);
+    hipLaunchKernelGGL(rtk::tile_scan_kernel, dim3(1), dim3(64), 0, stream, hist);
+    hipLaunchKernelGGL(rtk::tile_scatter_kernel, grid, dim3(256), 0, stream, cost, n, hist, order);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lanes_per_pixel) {
+    uint32_t bw = 16u, bh = 16u;  // 2*TW x 2*TH of the launch's shape
+    switch (lanes_per_pixel) {
+        case 16: bw = 2u * rtk::Shape<16>::TW; bh = 2u * rtk::Shape<16>::TH; break;
+        case 8: bw = 2u * rtk::Shape<8>::TW; bh = 2u * rtk::Shape<8>::TH; break;
+        case 4: bw = 2u * rtk::Shape<4>::TW; bh = 2u * rtk::Shape<4>::TH; break;
+        case 2: bw = 2u * rtk::Shape<2>::TW; bh = 2u * rtk::Shape<2>::TH; break;
+        default: bw = 2u * rtk::Shape<1>::TW; bh = 2u * rtk::Shape<1>::TH; break;
+    }
+    return ((width + bw - 1u) / bw) * ((local_rows + bh - 1u) / bh);
+}
 
 template <int P>
 static void launch_p(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream) {

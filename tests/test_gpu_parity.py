@@ -270,3 +270,28 @@ def test_cone_culling_is_exact_at_full_resolution(rt, orc, torch_cuda, monkeypat
     ref = out[(("RT_CULL", "0"), ("RT_LANES_PER_PIXEL", "4"))]
     for key, g in out.items():
         assert torch_cuda.equal(g[0], ref[0]) and torch_cuda.equal(g[1], ref[1]) and g[2] == ref[2], key
+
+
+@pytest.mark.parametrize("lpp", ["4", "16"])
+def test_tile_order_from_previous_launch_keeps_every_bit(rt, orc, torch_cuda, monkeypatch, lpp):
+    """Repeated launches of one geometry run their tiles heaviest-first (order
+    learned from the previous launch): the image, the accumulation and the ray
+    count must equal the identity-order launch bit for bit, launch after launch."""
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", lpp)
+    s, _ = _scenes(rt, orc, 1, 64)
+    W, H = 640, 360
+    cam = rt.camera_setup(s, W, H)
+    monkeypatch.setenv("RT_TILE_ORDER", "0")
+    dev0 = rt.Device(0)
+    try:
+        ref = gpu_render(rt, torch_cuda, dev0, s, cam, W, H, frames=6, bounces=8)
+    finally:
+        dev0.close()
+    monkeypatch.setenv("RT_TILE_ORDER", "1")
+    dev = rt.Device(0)
+    try:
+        for _ in range(4):
+            g = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=6, bounces=8)
+            assert torch_cuda.equal(g[0], ref[0]) and torch_cuda.equal(g[1], ref[1]) and g[2] == ref[2]
+    finally:
+        dev.close()
