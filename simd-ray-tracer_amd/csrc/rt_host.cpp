@@ -36,7 +36,7 @@ struct rt_device {
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
     int tile_sched = 1;
-    uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_hist = nullptr;
+    uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
     size_t tile_cap = 0;
     uint64_t tile_key = 0;
     bool tile_order_valid = false;
@@ -124,7 +124,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
     if (d->tile_stream_set) (void)hipStreamSynchronize(d->tile_stream);
     (void)hipFree(d->d_tile_cost);
     (void)hipFree(d->d_tile_order);
-    (void)hipFree(d->d_tile_hist);
+    (void)hipFree(d->d_tile_scratch);
     (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
@@ -421,11 +421,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(s));
             (void)hipFree(d->d_tile_cost);
             (void)hipFree(d->d_tile_order);
-            (void)hipFree(d->d_tile_hist);
-            d->d_tile_cost = d->d_tile_order = d->d_tile_hist = nullptr;
+            (void)hipFree(d->d_tile_scratch);
+            d->d_tile_cost = d->d_tile_order = d->d_tile_scratch = nullptr;
             if (hipMalloc(&d->d_tile_cost, n_tiles * 4u) != hipSuccess ||
                 hipMalloc(&d->d_tile_order, n_tiles * 4u) != hipSuccess ||
-                hipMalloc(&d->d_tile_hist, 64u * 4u) != hipSuccess)
+                hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(n_tiles)) != hipSuccess)
                 return fail(RT_ENOMEM, "rt_trace: tile order buffers");
             d->tile_cap = n_tiles;
             d->tile_key = ~key;
@@ -441,7 +441,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, lpp, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (sched) {
-        if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_hist, n_tiles, s) != 0)
+        if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
             return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
         d->tile_order_valid = true;
     }

@@ -53,7 +53,9 @@ extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull,
                                 hipStream_t stream);
 // Heaviest-first tile order for the next launch from this launch's costs
 // (resets the costs); n = rtk_tile_count(...) of the launch geometry.
-extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *hist, uint32_t n, hipStream_t stream);
+// scratch: rtk_tile_sort_scratch(n) bytes of device memory
+extern "C" size_t rtk_tile_sort_scratch(uint32_t n);
+extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *scratch, uint32_t n, hipStream_t stream);
 extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lanes_per_pixel);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

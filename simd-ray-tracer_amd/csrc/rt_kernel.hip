@@ -972,43 +972,128 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint8_t *src, uint6
 
 // ---- heaviest-first tile order for the next launch (counting sort of the
 // per-tile costs this launch measured into 32 log2 buckets, descending)
-__global__ __launch_bounds__(256) void tile_hist_kernel(const uint32_t *cost, uint32_t n, uint32_t *hist) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(hist + (31u - __builtin_clz(cost[i] | 1u)), 1u);
+// Counting sort of the tiles by log2(cost), heaviest bucket first, stable,
+// without atomics, over the whole grid (a single-block version was latency
+// bound at ~60 us; grid-wide device atomics on the few busy buckets ~300 us).
+// A wave walks its 64 tiles visiting only the distinct buckets present
+// (readlane of the first pending lane + ballot) and keeps per-bucket counters
+// in lane k of one VGPR.  Blocks cover 1024 tiles:
+//   tile_count_kernel: block j's 32 bucket counts -> bcount[32*j + k]
+//   tile_scan_kernel:  exclusive scan in (bucket descending, block ascending)
+//                      order, staged through LDS
+//   tile_rank_kernel:  per-wave bases inside the block, the walk again ->
+//                      order[rank] = tile
+// Consecutive ranks keep similar cost: blocks are dealt round-robin to the 8
+// XCDs, so alternating heavy and light tiles would put all heavy work on half
+// of them (measured 2x slower).
+constexpr uint32_t kSortBlock = 1024, kSortWaves = kSortBlock / 64, kScanLds = 16384;
+
+__device__ __forceinline__ uint32_t tile_bucket(const uint32_t *cost, uint32_t i, uint32_t n) {
+    return i < n ? 31u - __builtin_clz(cost[i] | 1u) : 32u;  // 32: past the end
 }
 
-__global__ void tile_scan_kernel(uint32_t *hist) {  // hist[0..31] -> start offsets, heavy buckets first
-    if (threadIdx.x != 0) return;
-    uint32_t off = 0;
-    for (int b = 31; b >= 0; --b) {
-        const uint32_t c = hist[b];
-        hist[b] = off;
-        hist[32 + b] = 0;  // scatter cursor
-        off += c;
+// lane k < 32 of the result: run[k] + (this wave's count of bucket k);
+// *rank: run[b] + this lane's position among the wave's lanes with bucket b
+__device__ __forceinline__ uint32_t wave_walk(uint32_t b, uint32_t run, uint32_t lane, uint32_t *rank) {
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t pend = b;
+    for (uint64_t live = __ballot(pend < 32u); live; live = __ballot(pend < 32u)) {
+        const uint32_t b0 = __builtin_amdgcn_readlane(pend, (int)__builtin_ctzll(live));
+        const uint64_t m = __ballot(pend == b0);
+        if (pend == b0) {
+            *rank = __builtin_amdgcn_readlane(run, (int)b0) + (uint32_t)__popcll(m & lt);
+            pend = 32u;
+        }
+        if (lane == b0) run += (uint32_t)__popcll(m);
+    }
+    return run;
+}
+
+__global__ __launch_bounds__(kSortBlock) void tile_count_kernel(const uint32_t *cost, uint32_t n, uint32_t *bcount) {
+    __shared__ uint32_t wc[kSortWaves][32];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t rank;
+    const uint32_t c = wave_walk(tile_bucket(cost, blockIdx.x * kSortBlock + threadIdx.x, n), 0u, lane, &rank);
+    if (lane < 32) wc[wave][lane] = c;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kSortWaves; ++w) t += wc[w][threadIdx.x];
+        bcount[32u * blockIdx.x + threadIdx.x] = t;
     }
 }
 
-__global__ __launch_bounds__(256) void tile_scatter_kernel(uint32_t *cost, uint32_t n, uint32_t *hist,
-                                                           uint32_t *order) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = 31u - __builtin_clz(cost[i] | 1u);
-    const uint32_t r = hist[b] + atomicAdd(hist + 32 + b, 1u);  // rank, heaviest first
-    // (consecutive blocks must stay of similar cost: blocks are dealt
-    // round-robin to the 8 XCDs, so alternating heavy and light tiles would
-    // put all heavy work on half of them -- measured 2x slower)
-    order[r] = i;
-    cost[i] = 0;  // measured afresh by the next launch
+__global__ __launch_bounds__(1024) void tile_scan_kernel(uint32_t *bcount, uint32_t n_blk) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t stage[kScanLds];
+    const uint32_t len = 32u * n_blk, t = threadIdx.x, per = (len + 1023u) / 1024u;
+    const bool in_lds = len <= kScanLds;
+    if (in_lds)
+        for (uint32_t j = t; j < len; j += 1024u) stage[j] = bcount[j];
+    __syncthreads();
+    uint32_t *const src = in_lds ? stage : bcount;
+    // scan position p -> (bucket 31 - p / n_blk, block p % n_blk)
+    auto at = [&](uint32_t p) -> uint32_t & { return src[32u * (p % n_blk) + (31u - p / n_blk)]; };
+    const uint32_t p0 = min(len, t * per), p1 = min(len, p0 + per);
+    uint32_t sum = 0;
+    for (uint32_t p = p0; p < p1; ++p) sum += at(p);
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {  // inclusive Hillis-Steele scan of the partials
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t off = part[t] - sum;
+    for (uint32_t p = p0; p < p1; ++p) {
+        const uint32_t c = at(p);
+        at(p) = off;
+        off += c;
+    }
+    __syncthreads();
+    if (in_lds)
+        for (uint32_t j = t; j < len; j += 1024u) bcount[j] = stage[j];
+}
+
+__global__ __launch_bounds__(kSortBlock) void tile_rank_kernel(uint32_t *cost, uint32_t n, const uint32_t *bbase,
+                                                               uint32_t *order) {
+    __shared__ uint32_t wc[kSortWaves][32];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * kSortBlock + threadIdx.x, b = tile_bucket(cost, i, n);
+    uint32_t rank = 0;
+    const uint32_t c = wave_walk(b, 0u, lane, &rank);
+    if (lane < 32) wc[wave][lane] = c;
+    __syncthreads();
+    if (threadIdx.x < 32) {  // the block's base -> each wave's base, in wave order
+        uint32_t off = bbase[32u * blockIdx.x + threadIdx.x];
+        for (uint32_t w = 0; w < kSortWaves; ++w) {
+            const uint32_t x = wc[w][threadIdx.x];
+            wc[w][threadIdx.x] = off;
+            off += x;
+        }
+    }
+    __syncthreads();
+    (void)wave_walk(b, lane < 32 ? wc[wave][lane] : 0u, lane, &rank);
+    if (b < 32u) {
+        order[rank] = i;
+        cost[i] = 0;  // measured afresh by the next launch
+    }
 }
 
 }  // namespace rtk
 
-extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *hist, uint32_t n, hipStream_t stream) {
-    (void)hipMemsetAsync(hist, 0, 64 * sizeof(uint32_t), stream);
-    const dim3 grid((n + 255u) / 256u);
-    hipLaunchKernelGGL(rtk::tile_hist_kernel, grid, dim3(256), 0, stream, (const uint32_t *)cost, n, hist);
-    hipLaunchKernelGGL(rtk::tile_scan_kernel, dim3(1), dim3(64), 0, stream, hist);
-    hipLaunchKernelGGL(rtk::tile_scatter_kernel, grid, dim3(256), 0, stream, cost, n, hist, order);
+extern "C" size_t rtk_tile_sort_scratch(uint32_t n) {
+    return 32u * 4u * (size_t)((n + rtk::kSortBlock - 1u) / rtk::kSortBlock);
+}
+
+extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *scratch, uint32_t n, hipStream_t stream) {
+    const uint32_t n_blk = (n + rtk::kSortBlock - 1u) / rtk::kSortBlock;
+    if (n_blk == 0) return 0;
+    const dim3 grid(n_blk), block(rtk::kSortBlock);
+    hipLaunchKernelGGL(rtk::tile_count_kernel, grid, block, 0, stream, (const uint32_t *)cost, n, scratch);
+    hipLaunchKernelGGL(rtk::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, scratch, n_blk);
+    hipLaunchKernelGGL(rtk::tile_rank_kernel, grid, block, 0, stream, cost, n, (const uint32_t *)scratch, order);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
