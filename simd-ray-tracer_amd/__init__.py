@@ -281,7 +281,9 @@ class Device:
         _check(rc, "rt_debug_stats")
         if rc == 0:
             return None
-        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups"]
+        keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups",
+                "sec_sparse_iters", "sec_sparse_lanes", "sec_tail_iters", "pri_cycles", "sec_cycles",
+                "fold_cycles", "init_cycles", "cull_cycles", "sync_cycles", "post_cycles"]
         return {k: int(v) for k, v in zip(keys, out) if not k.startswith("_")}
 
     def debug_wave_times(self, max_waves: int = 1 << 22):

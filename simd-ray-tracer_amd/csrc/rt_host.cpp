@@ -37,9 +37,16 @@ struct rt_device {
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
     int tile_sched = 1;
     uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
-    size_t tile_cap = 0;
-    uint64_t tile_key = 0;
+    uint32_t *d_tile_live = nullptr;
+    unsigned long long *d_cull_counters = nullptr;  // 2 x 64 striped counters of the cull pass
+    uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
+    size_t tile_cap = 0, mask_cap = 0;
+    // the launch (camera, scene, geometry) the masks / live list / order were made for
+    std::vector<uint32_t> tile_key;
     bool tile_order_valid = false;
+    uint32_t n_live = 0;
+    uint64_t dead_pixels = 0;
+    uint64_t scene_gen = 0;  // bumped by every rt_scene_upload
     hipStream_t tile_stream = nullptr;
     bool tile_stream_set = false;
     uint32_t cu_count = 256;
@@ -95,7 +102,7 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     const char *pf = getenv("RT_PREFILTER");  // secondary-ray prefilter: 0 off, 1 on, unset = per-scene auto
     if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
     const char *to = getenv("RT_TILE_ORDER");
-    if (to && to[0] == '0') d->tile_sched = 0;
+    if (to && (to[0] == '0' || to[0] == '2')) d->tile_sched = to[0] - '0';  // 2: also for P = 16
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -125,6 +132,9 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_tile_cost);
     (void)hipFree(d->d_tile_order);
     (void)hipFree(d->d_tile_scratch);
+    (void)hipFree(d->d_tile_live);
+    (void)hipFree(d->d_cull_counters);
+    (void)hipFree(d->d_masks);
     (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
@@ -301,6 +311,7 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     d->n_spheres = scene->ScalarSpheres.Count;
     d->use_sky = scene->UseSkyColor;
     d->scene_set = true;
+    d->scene_gen += 1;
     return RT_OK;
 }
 
@@ -400,47 +411,101 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         lpp = pixels >= (uint64_t)d->cu_count * 3072u ? 4 : 8;
         while (lpp > 1 && (uint32_t)lpp / 2u >= desc->Frames) lpp /= 2;
     }
-    uint32_t n_tiles = 0;
-    // heaviest-first tile order: measured faster for 4 and 8 lanes per pixel,
-    // slower for 16 (identity order kept there)
-    const bool sched = d->tile_sched && lpp <= 8;
-    if (sched) {
-        // the order is a block -> tile map: only valid for the same launch
-        // geometry, and only once the sort that wrote it has run (same stream)
-        n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
-        const uint64_t key = ((uint64_t)desc->Width << 40) ^ ((uint64_t)local_rows << 20) ^ ((uint64_t)lpp << 14) ^
-                             ((uint64_t)band_rows << 8) ^ ((uint64_t)band_count << 4) ^ desc->BandIndex ^
-                             ((uint64_t)n_tiles << 32);
-        if (!d->tile_stream_set || s != d->tile_stream) {
-            if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(d->tile_stream));
-            d->tile_stream = s;
-            d->tile_stream_set = true;
-            d->tile_order_valid = false;
+    // Tile scheduling.  Block tiles (2TW x 2TH pixels) are traced in the order
+    // tile_order[0 .. n_live): with culling, the cull pass (once per camera /
+    // scene / geometry) writes every wave tile's primary group mask and a
+    // live-first order, and dead tiles (no candidate group anywhere, no sky)
+    // never reach the trace kernel -- rtk_launch_empty folds their pixels.
+    // With heaviest-first scheduling each launch also measures its tiles and
+    // re-sorts them for the next launch (live tiles keep costs > 0, dead ones
+    // 0, so the live prefix is preserved).
+    const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
+    const uint32_t n_words = (a.n_groups + 63u) / 64u;
+    const bool cull = d->cull != 0;
+    const bool empty_capable = cull && !d->use_sky && desc->MaxBounce != 0;
+    const bool sched = d->tile_sched == 2 || (d->tile_sched && lpp <= 8);
+    a.tiles_x = rtk_tiles_x(desc->Width, lpp);
+    std::vector<uint32_t> key = {desc->Width, desc->Height, local_rows, band_rows, band_count, desc->BandIndex,
+                                 (uint32_t)lpp, (uint32_t)rs, (uint32_t)cull, (uint32_t)empty_capable, (uint32_t)sched,
+                                 (uint32_t)d->scene_gen, (uint32_t)(d->scene_gen >> 32)};
+    for (const float *f : {a.cam_pos, a.cam_x, a.cam_y, a.film_center}) {
+        for (int i = 0; i < 3; ++i) {
+            uint32_t u;
+            memcpy(&u, f + i, 4);
+            key.push_back(u);
         }
-        if (n_tiles > d->tile_cap) {
-            if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(s));
-            (void)hipFree(d->d_tile_cost);
-            (void)hipFree(d->d_tile_order);
-            (void)hipFree(d->d_tile_scratch);
-            d->d_tile_cost = d->d_tile_order = d->d_tile_scratch = nullptr;
-            if (hipMalloc(&d->d_tile_cost, n_tiles * 4u) != hipSuccess ||
-                hipMalloc(&d->d_tile_order, n_tiles * 4u) != hipSuccess ||
-                hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(n_tiles)) != hipSuccess)
-                return fail(RT_ENOMEM, "rt_trace: tile order buffers");
-            d->tile_cap = n_tiles;
-            d->tile_key = ~key;
-        }
-        if (key != d->tile_key) {
-            HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_tiles * 4u, s));
-            d->tile_key = key;
-            d->tile_order_valid = false;
-        }
-        a.tile_cost = d->d_tile_cost;
-        a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
     }
-    if (rtk_launch_trace(&a, desc->EnableSIMD ? 1 : 0, d->src, d->cull, lpp, s) != 0)
+    for (const float f : {a.film_w, a.film_h}) {
+        uint32_t u;
+        memcpy(&u, &f, 4);
+        key.push_back(u);
+    }
+    if (!d->tile_stream_set || s != d->tile_stream) {
+        // order and masks are written and read in stream order
+        if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(d->tile_stream));
+        d->tile_stream = s;
+        d->tile_stream_set = true;
+        d->tile_key.clear();
+    }
+    if (n_tiles > d->tile_cap) {
+        HIP_OK(hipStreamSynchronize(s));
+        for (uint32_t **b : {&d->d_tile_cost, &d->d_tile_order, &d->d_tile_scratch, &d->d_tile_live}) {
+            (void)hipFree(*b);
+            *b = nullptr;
+        }
+        if (hipMalloc(&d->d_tile_cost, n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_order, n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(n_tiles)) != hipSuccess)
+            return fail(RT_ENOMEM, "rt_trace: tile order buffers");
+        if (!d->d_cull_counters && hipMalloc(&d->d_cull_counters, 128u * 8u) != hipSuccess)
+            return fail(RT_ENOMEM, "rt_trace: tile order buffers");
+        d->tile_cap = n_tiles;
+        d->tile_key.clear();
+    }
+    const size_t mask_words = (size_t)n_tiles * 4u * n_words;
+    if (cull && mask_words > d->mask_cap) {
+        HIP_OK(hipStreamSynchronize(s));
+        (void)hipFree(d->d_masks);
+        d->d_masks = nullptr;
+        if (hipMalloc(&d->d_masks, mask_words * 8u) != hipSuccess) return fail(RT_ENOMEM, "rt_trace: cull masks");
+        d->mask_cap = mask_words;
+        d->tile_key.clear();
+    }
+    if (key != d->tile_key) {
+        d->tile_key = key;
+        if (cull) {
+            a.masks = d->d_masks;
+            if (rtk_launch_cull(&a, lpp, d->d_tile_live, d->d_tile_cost, d->d_cull_counters, empty_capable ? 1 : 0, s) !=
+                    0 ||
+                rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
+                return fail(RT_EIO, "rt_trace: cull pass launch failed: %s", hipGetErrorString(hipGetLastError()));
+            unsigned long long c[128];
+            HIP_OK(hipMemcpyAsync(c, d->d_cull_counters, sizeof(c), hipMemcpyDeviceToHost, s));
+            HIP_OK(hipStreamSynchronize(s));
+            d->n_live = 0;
+            d->dead_pixels = 0;
+            for (int i = 0; i < 64; ++i) {
+                d->n_live += (uint32_t)c[i];
+                d->dead_pixels += c[64 + i];
+            }
+            d->tile_order_valid = true;
+        } else {
+            HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_tiles * 4u, s));
+            d->n_live = n_tiles;
+            d->dead_pixels = 0;
+            d->tile_order_valid = false;  // identity until a measured sort exists
+        }
+    }
+    a.masks = cull ? d->d_masks : nullptr;
+    a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
+    a.tile_cost = sched ? d->d_tile_cost : nullptr;
+    if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, d->src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (sched) {
+    if (empty_capable && d->n_live < n_tiles &&
+        rtk_launch_empty(&a, lpp, d->d_tile_live, (unsigned long long)(d->dead_pixels * desc->Frames), s) != 0)
+        return fail(RT_EIO, "rt_trace: empty-tile launch failed: %s", hipGetErrorString(hipGetLastError()));
+    if (sched && d->n_live > 0) {
         if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
             return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
         d->tile_order_valid = true;

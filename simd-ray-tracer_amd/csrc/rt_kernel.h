@@ -39,9 +39,12 @@ struct TraceArgs {
     unsigned long long *wave_times;  // optional (RT_WAVETIMES): per-wave {start, end} s_memrealtime
     const uint32_t *tile_order;  // optional: block -> tile map (heaviest first), NULL = identity
     uint32_t *tile_cost;         // optional: per-tile cost (max wave shader cycles), atomicMax'd
+    const uint64_t *masks;       // CULL: per wave tile (4*tile + wave) n_words primary group masks
+    uint32_t tiles_x;            // block tiles per row (2TW x 2TH pixels each)
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
-       kStatCount = 16 };
+       kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
+       kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatCount = 16 };
 
 // Dynamic LDS per block: rsqrt table + fold table + groups + materials.
 static inline size_t rtk_lds_bytes(uint32_t n_groups) {
@@ -57,5 +60,21 @@ extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull,
 extern "C" size_t rtk_tile_sort_scratch(uint32_t n);
 extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *scratch, uint32_t n, hipStream_t stream);
 extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lanes_per_pixel);
+extern "C" uint32_t rtk_tiles_x(uint32_t width, int lanes_per_pixel);
+// grid: blocks of the trace launch (tile_order[0..grid) when tile_order is set)
+extern "C" int rtk_launch_trace_grid(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
+                                     uint32_t grid, hipStream_t stream);
+// Primary-ray cone culling of every wave tile -> a->masks (must be set);
+// per block tile live[t] (some wave tile has a candidate group, or
+// !empty_capable) and cost[t] = live ? 2 : 0 (so a tile sort puts live tiles
+// first); counters[0, 64) sum to the live tiles, counters[64, 128) to the
+// image pixels of dead tiles (zeroed by the call).
+extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t *live, uint32_t *cost,
+                               unsigned long long *counters, int empty_capable, hipStream_t stream);
+// Pixels of dead block tiles (live[t] == 0): every sample misses with no sky,
+// so fold zeros into the running mean, store both images; adds dead_rays
+// (dead pixels x frames) to the ray counter once.
+extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
+                                unsigned long long dead_rays, hipStream_t stream);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

@@ -635,6 +635,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
     constexpr uint32_t kRing = Ring<P>::N;
     extern __shared__ float4 smem[];
+    const uint64_t st_entry = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
     __shared__ uint64_t s_mask[kWavesPerBlock][kMaxMaskWords];
@@ -666,9 +667,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     // Tile of this block: heaviest-first order from the previous launch's
     // measured per-tile cost when the host supplies one (tile_order), so the
     // long tiles do not start last and form the launch's tail.
-    const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t blk = blockIdx.x;
     const uint32_t tile = a.tile_order ? a.tile_order[blk] : blk;
-    const uint32_t tile_x = tile % gridDim.x, tile_y = tile / gridDim.x;
+    const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
     const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t x0 = tile_x * (2u * TW) + (wave & 1u) * TW;
     const uint32_t ly0 = tile_y * (2u * TH) + (wave >> 1) * TH;
@@ -681,33 +682,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     float4 *ring = s_ring + wave * kRing * kRingStride + pl;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
-    if (CULL) {
-        // the wave's tile; band_rows % 8 == 0 keeps its TH rows contiguous
-        const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
-        const Cone c = tile_cone(a, (double)x0 - 0.501, (double)(x0 + TW - 1u) + 0.501, (double)y0 - 0.501,
-                                 (double)(y0 + TH - 1u) + 0.501);
-        // one sphere per lane (64 per ballot), folded into one bit per group
-        const float *gf = reinterpret_cast<const float *>(a.groups);
-        for (uint32_t w = 0; w < n_words; ++w) {
-            uint64_t gm = 0;
-            for (uint32_t q = 0; q < 4u && (w * 64u + q * 16u) < a.n_groups; ++q) {
-                const uint32_t sph = (w * 64u + q * 16u) * 4u + lane;  // sphere slot 4*g + l
-                bool cand = false;
-                if (sph < 4u * a.n_groups) {
-                    const float *row = gf + (size_t)(sph >> 2) * (4u * kGroupF4) + (sph & 3u);
-                    cand = cone_may_hit(a, c, row[4u * kRowX], row[4u * kRowY], row[4u * kRowZ], row[4u * kRowR2]);
-                }
-                uint64_t m = __ballot(cand);
-                m |= (m >> 1) | (m >> 2) | (m >> 3);  // bit 4i: some sphere of group 16q+i
-                uint64_t bits = 0;
-#pragma unroll
-                for (uint32_t i = 0; i < 16u; ++i) bits |= ((m >> (4u * i)) & 1u) << i;
-                gm |= bits << (16u * q);
-            }
-            if (lane == 0) s_mask[wave][w] = gm;
-        }
-    }
+    // the wave tile's primary group mask, from the cull pass (rtk_launch_cull)
+    if (CULL && lane < n_words) s_mask[wave][lane] = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
+    const uint64_t st_c1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
+    const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
 
     float accx = 0.0f, accy = 0.0f, accz = 0.0f;
     if (valid && owner && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
@@ -723,6 +702,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
     uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
+    uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
+    uint64_t st_cyc_pri = 0, st_cyc_sec = 0, st_cyc_fold = 0, st_cyc_setup = 0;
+    uint64_t st_cyc_cull = 0, st_cyc_sync = 0, st_cyc_post = 0;
     Sample p;
     p.bounce = 0;
     p.cx = p.cy = p.cz = 0.0f;
@@ -756,6 +738,13 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         mode = 2u;
     }
 
+    if (kStats && a.stats) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        st_cyc_setup = t_cost0 - st_entry;  // LDS image loads issued, tile picked
+        st_cyc_cull = st_c1 - t_cost0;
+        st_cyc_sync = st_c2 - st_c1;
+        st_cyc_post = t - st_c2;
+    }
     for (;;) {
         // ring space: sample k may start once k < folded + kRing (the oldest
         // unfolded sample's lane is never blocked, so this cannot deadlock)
@@ -770,12 +759,15 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         const uint64_t sec = __ballot(mode == 1u);
         const uint64_t alive = __ballot(mode != 2u || (owner && valid && folded < a.frames));
         if (alive == 0) break;
+        const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
         if ((pri | sec) != 0) {
             // Secondary segments run the full sphere loop; let them gather until
             // enough lanes share one (or no primary work is ready).
             const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
             if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
+                if (do_sec && __builtin_popcountll(sec) < 16) { st_sparse_it += 1; st_sparse_lanes += __builtin_popcountll(sec); }
+                if (do_sec && __ballot(mode == 0u) == 0) st_tail_it += 1;  // no samples left to start at all
                 else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
             }
             const bool traces = do_sec ? mode == 1u : can_start;
@@ -894,6 +886,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 }
             }
         }
+        const uint64_t st_t1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
+        if (kStats && a.stats && (pri | sec) != 0) {
+            const bool was_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+            (was_sec ? st_cyc_sec : st_cyc_pri) += st_t1 - st_t0;
+        }
         if (P > 1 && owner && valid) {
             // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
             // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
@@ -918,6 +915,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 }
             }
         }
+        if (kStats && a.stats) st_cyc_fold += __builtin_amdgcn_s_memtime() - st_t1;
     }
 
     if (valid && owner && a.frames > 0) {
@@ -945,7 +943,142 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatSecLanes, (unsigned long long)st_sec_lanes);
         atomicAdd(a.stats + kStatPriGroups, (unsigned long long)st_groups);
         atomicAdd(a.stats + kStatSecHitGroups, (unsigned long long)st_sec_hit);
+        atomicAdd(a.stats + kStatSecSparseIters, (unsigned long long)st_sparse_it);
+        atomicAdd(a.stats + kStatSecSparseLanes, (unsigned long long)st_sparse_lanes);
+        atomicAdd(a.stats + kStatSecTailIters, (unsigned long long)st_tail_it);
+        atomicAdd(a.stats + kStatPriCycles, (unsigned long long)st_cyc_pri);
+        atomicAdd(a.stats + kStatSecCycles, (unsigned long long)st_cyc_sec);
+        atomicAdd(a.stats + kStatFoldCycles, (unsigned long long)st_cyc_fold);
+        atomicAdd(a.stats + kStatSetupCycles, (unsigned long long)st_cyc_setup);
+        atomicAdd(a.stats + kStatCullCycles, (unsigned long long)st_cyc_cull);
+        atomicAdd(a.stats + kStatSyncCycles, (unsigned long long)st_cyc_sync);
+        atomicAdd(a.stats + kStatPostCycles, (unsigned long long)st_cyc_post);
     }
+}
+
+// Primary-ray culling of one wave tile (TW x TH pixels at x0, ly0): bit g of
+// the mask is set when some sphere of group g may pass some primary ray's
+// exact test (cone_may_hit).  One sphere per lane, 64 per ballot, folded
+// into one bit per group; word w covers groups 64w .. 64w+63.
+template <int P>
+__device__ __forceinline__ uint64_t wave_tile_mask(const TraceArgs &a, const Cone &c, uint32_t w, uint32_t lane) {
+    const float *gf = reinterpret_cast<const float *>(a.groups);
+    uint64_t gm = 0;
+    for (uint32_t q = 0; q < 4u && (w * 64u + q * 16u) < a.n_groups; ++q) {
+        const uint32_t sph = (w * 64u + q * 16u) * 4u + lane;  // sphere slot 4*g + l
+        bool cand = false;
+        if (sph < 4u * a.n_groups) {
+            const float *row = gf + (size_t)(sph >> 2) * (4u * kGroupF4) + (sph & 3u);
+            cand = cone_may_hit(a, c, row[4u * kRowX], row[4u * kRowY], row[4u * kRowZ], row[4u * kRowR2]);
+        }
+        uint64_t m = __ballot(cand);
+        m |= (m >> 1) | (m >> 2) | (m >> 3);  // bit 4i: some sphere of group 16q+i
+        uint64_t bits = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 16u; ++i) bits |= ((m >> (4u * i)) & 1u) << i;
+        gm |= bits << (16u * q);
+    }
+    return gm;
+}
+
+// The cull pass: one block per block tile, one wave per wave tile (the trace
+// kernel's geometry).  Runs once per camera / scene / launch geometry; the
+// trace launches reuse its masks and live-tile list.
+// Striped launch counters of the cull pass (one atomic per block tile, spread
+// over kCullStripes addresses so they do not serialise on one): [0, 64) live
+// block tiles, [64, 128) image pixels of dead block tiles.
+constexpr uint32_t kCullStripes = 64;
+
+// The cull pass: one block per block tile, one wave per wave tile (the trace
+// kernel's geometry).  Runs once per camera / scene / launch geometry; the
+// trace launches reuse its masks and live-tile list.
+template <int P>
+__global__ __launch_bounds__(256) void cull_kernel(TraceArgs a, uint32_t *live, uint32_t *cost,
+                                                   unsigned long long *counters, uint32_t empty_capable) {
+    constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH;
+    __shared__ uint32_t s_any;
+    const uint32_t tile = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
+    const uint32_t x0 = tile_x * (2u * TW) + (wave & 1u) * TW;
+    const uint32_t ly0 = tile_y * (2u * TH) + (wave >> 1) * TH;
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    // the wave's tile; band_rows % 8 == 0 keeps its TH rows contiguous
+    const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
+    const Cone c = tile_cone(a, (double)x0 - 0.501, (double)(x0 + TW - 1u) + 0.501, (double)y0 - 0.501,
+                             (double)(y0 + TH - 1u) + 0.501);
+    const uint32_t n_words = (a.n_groups + 63u) / 64u;
+    bool any = false;
+    for (uint32_t w = 0; w < n_words; ++w) {
+        const uint64_t gm = wave_tile_mask<P>(a, c, w, lane);
+        if (lane == 0) const_cast<uint64_t *>(a.masks)[((size_t)tile * 4u + wave) * n_words + w] = gm;
+        any = any || gm != 0;
+    }
+    // a wave tile entirely outside the image does no work
+    if (lane == 0 && any && x0 < a.width && ly0 < a.local_rows) atomicOr(&s_any, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const bool l = s_any != 0 || !empty_capable;
+        live[tile] = l ? 1u : 0u;
+        cost[tile] = l ? 2u : 0u;
+        const uint32_t stripe = tile % kCullStripes;
+        if (l) {
+            atomicAdd(counters + stripe, 1ull);
+        } else {
+            const uint32_t bx = tile_x * 2u * TW, by = tile_y * 2u * TH;
+            const uint32_t w = min(2u * TW, a.width - bx), h = min(2u * TH, a.local_rows - by);
+            atomicAdd(counters + kCullStripes + stripe, (unsigned long long)w * h);
+        }
+    }
+}
+
+// Pixels of dead block tiles: no sphere group passes any of the tile's
+// (conservative) cone tests, so every primary ray of every sample misses;
+// without a sky term each sample's Out is exactly 0 (main.cpp:433-440), its
+// one segment still counts (main.cpp:390; dead_rays = dead pixels x frames
+// from the cull pass, added once), and its blend is
+// Final = 0*(1/n) + Prev*((n-1)/n) = RN(Prev*((n-1)/n)) -- folded here without
+// generating the rays (an all-zero running mean stays exactly zero).  The
+// ratios are the trace kernel's fold-table values.
+template <int P>
+__global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t *live, unsigned long long dead_rays) {
+    constexpr uint32_t BW = 2u * Shape<P>::TW, BH = 2u * Shape<P>::TH;
+    __shared__ float ratio[kFoldTable];
+    const bool fold = a.prev_count > 0 && !(a.flags & kFlagAccumZero);
+    if (fold)
+        for (uint32_t i = threadIdx.x; i < kFoldTable; i += blockDim.x) {
+            const uint32_t pc = a.prev_count + i;
+            ratio[i] = (float)pc / (float)(pc + 1u);
+        }
+    __syncthreads();
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && dead_rays) atomicAdd(a.rays, dead_rays);
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x, ly = blockIdx.y;
+    if (!(x < a.width && live[(ly / BH) * a.tiles_x + x / BW] == 0u)) return;
+    const size_t pix = (size_t)ly * a.width + x;
+    float accx = 0.0f, accy = 0.0f, accz = 0.0f;
+    if (fold) {
+        const float4 pv = a.prev[pix];
+        accx = pv.x;
+        accy = pv.y;
+        accz = pv.z;
+    }
+    if (accx != 0.0f || accy != 0.0f || accz != 0.0f) {
+        for (uint32_t q = 0; q < a.frames; ++q) {
+            float r;
+            if (q < kFoldTable) {
+                r = ratio[q];
+            } else {
+                const uint32_t pc = a.prev_count + q;
+                r = (float)pc / (float)(pc + 1u);
+            }
+            accx = 0.0f + accx * r;
+            accy = 0.0f + accy * r;
+            accz = 0.0f + accz * r;
+        }
+    }
+    a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
+    a.cur[pix] = to_u8(linear_to_srgb(accx)) | (to_u8(linear_to_srgb(accy)) << 8) |
+                 (to_u8(linear_to_srgb(accz)) << 16) | (255u << 24);
 }
 
 // Scatter RCCL-gathered compact band images into the full framebuffer.
@@ -1097,6 +1230,10 @@ extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *s
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+extern "C" uint32_t rtk_tiles_x(uint32_t width, int lanes_per_pixel) {
+    return rtk_tile_count(width, 1u, lanes_per_pixel);
+}
+
 extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lanes_per_pixel) {
     uint32_t bw = 16u, bh = 16u;  // 2*TW x 2*TH of the launch's shape
     switch (lanes_per_pixel) {
@@ -1110,10 +1247,8 @@ extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lane
 }
 
 template <int P>
-static void launch_p(const TraceArgs *a, int simd, int src, int cull, hipStream_t stream) {
-    constexpr uint32_t BW = 2u * rtk::Shape<P>::TW, BH = 2u * rtk::Shape<P>::TH;
-    const dim3 block(256);
-    const dim3 grid((a->width + BW - 1u) / BW, (a->local_rows + BH - 1u) / BH);
+static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks, hipStream_t stream) {
+    const dim3 block(256), grid(n_blocks);
     const size_t lds = rtk_lds_bytes(a->n_groups);
 #define RTK_LAUNCH(S, R, C) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P>), grid, block, lds, stream, *a)
     const int key = (simd ? 4 : 0) | (src == kSrcLds ? 2 : 0) | (cull ? 1 : 0);
@@ -1130,17 +1265,63 @@ static void launch_p(const TraceArgs *a, int simd, int src, int cull, hipStream_
 #undef RTK_LAUNCH
 }
 
-extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
-                                hipStream_t stream) {
+extern "C" int rtk_launch_trace_grid(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
+                                     uint32_t n_blocks, hipStream_t stream) {
+    if (n_blocks == 0) return 0;
     switch (lanes_per_pixel) {
-        case 16: launch_p<16>(a, simd, src, cull, stream); break;
-        case 8: launch_p<8>(a, simd, src, cull, stream); break;
-        case 4: launch_p<4>(a, simd, src, cull, stream); break;
-        case 2: launch_p<2>(a, simd, src, cull, stream); break;
-        default: launch_p<1>(a, simd, src, cull, stream); break;
+        case 16: launch_p<16>(a, simd, src, cull, n_blocks, stream); break;
+        case 8: launch_p<8>(a, simd, src, cull, n_blocks, stream); break;
+        case 4: launch_p<4>(a, simd, src, cull, n_blocks, stream); break;
+        case 2: launch_p<2>(a, simd, src, cull, n_blocks, stream); break;
+        default: launch_p<1>(a, simd, src, cull, n_blocks, stream); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
+                                hipStream_t stream) {
+    return rtk_launch_trace_grid(a, simd, src, cull, lanes_per_pixel,
+                                 rtk_tile_count(a->width, a->local_rows, lanes_per_pixel), stream);
+}
+
+#define RTK_BY_P(F, ...)                                     \
+    switch (lanes_per_pixel) {                               \
+        case 16: F<16>(__VA_ARGS__); break;                  \
+        case 8: F<8>(__VA_ARGS__); break;                    \
+        case 4: F<4>(__VA_ARGS__); break;                    \
+        case 2: F<2>(__VA_ARGS__); break;                    \
+        default: F<1>(__VA_ARGS__); break;                   \
+    }
+
+template <int P>
+static void launch_cull_p(const TraceArgs *a, uint32_t *live, uint32_t *cost, unsigned long long *counters,
+                          int empty_capable, hipStream_t stream) {
+    const uint32_t n = rtk_tile_count(a->width, a->local_rows, P);
+    (void)hipMemsetAsync(counters, 0, 2u * rtk::kCullStripes * sizeof(unsigned long long), stream);
+    hipLaunchKernelGGL(rtk::cull_kernel<P>, dim3(n), dim3(256), 0, stream, *a, live, cost, counters,
+                       (uint32_t)(empty_capable != 0));
+}
+
+extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t *live, uint32_t *cost,
+                               unsigned long long *counters, int empty_capable, hipStream_t stream) {
+    if (!a->masks) return -1;
+    RTK_BY_P(launch_cull_p, a, live, cost, counters, empty_capable, stream)
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+template <int P>
+static void launch_empty_p(const TraceArgs *a, const uint32_t *live, unsigned long long dead_rays,
+                           hipStream_t stream) {
+    hipLaunchKernelGGL(rtk::empty_kernel<P>, dim3((a->width + 255u) / 256u, a->local_rows), dim3(256), 0, stream, *a,
+                       live, dead_rays);
+}
+
+extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
+                                unsigned long long dead_rays, hipStream_t stream) {
+    RTK_BY_P(launch_empty_p, a, live, dead_rays, stream)
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+#undef RTK_BY_P
 
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream) {

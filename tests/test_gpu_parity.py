@@ -295,3 +295,30 @@ def test_tile_order_from_previous_launch_keeps_every_bit(rt, orc, torch_cuda, mo
             assert torch_cuda.equal(g[0], ref[0]) and torch_cuda.equal(g[1], ref[1]) and g[2] == ref[2]
     finally:
         dev.close()
+
+
+def test_dead_tiles_fold_a_nonzero_running_mean(rt, orc, torch_cuda, gdev):
+    """Pixels of tiles no primary ray can hit go through rtk_launch_empty; with a
+    random non-zero accumulation (PreviousRayCount 5) they must blend zeros
+    exactly like the oracle's traced misses."""
+    s, o = _scenes(rt, orc, 1, 64)
+    W, H = 256, 192
+    cam = rt.camera_setup(s, W, H)
+    rng = np.random.default_rng(11)
+    prev_np = rng.uniform(0.0, 2.0, (W * H, 4)).astype(np.float32)
+    prev = torch_cuda.from_numpy(prev_np.copy()).to("cuda")
+    g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=3, bounces=4, prev_count=5, prev=prev)
+    r = orc.render(o, orc.camera(o, W, H), W, H, prev_count=5, frames=3, max_bounce=4, prev=prev_np.copy())
+    assert_same(*g, *r)
+
+
+def test_camera_change_recomputes_the_cull_pass(rt, orc, torch_cuda, gdev):
+    """The cull masks and live-tile list are cached per camera / scene /
+    geometry: moving the camera between launches on one device must re-cull."""
+    s, o = _scenes(rt, orc, 1, 64)
+    W, H = 128, 96
+    for dist, ang in [(None, None), (6.0, 0.7), (None, None)]:
+        cam = rt.camera_setup(s, W, H, distance=dist, x_angle=ang)
+        g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5)
+        r = orc.render(o, orc.camera(o, W, H, distance=dist, x_angle=ang), W, H, frames=2, max_bounce=5)
+        assert_same(*g, *r)
