@@ -198,7 +198,12 @@ uint32_t rt_band_local_rows(uint32_t height, uint32_t band_rows, uint32_t band_c
  * cam->PreviousImage.Data are DEVICE pointers to compact band-local images
  * (rt_band_local_rows x Width).  `d_rays` (device u64) is incremented by
  * the bounce segments traced (RaysCastInThread, main.cpp:390).
- * Asynchronous on `stream` (hipStream_t; NULL = the HIP null stream). */
+ * Asynchronous on `stream` (hipStream_t; NULL = the HIP null stream), except
+ * that the first launch for a new camera / scene / geometry on this device
+ * runs the primary-ray cull pass and waits for its live-tile count (one
+ * stream synchronisation); later launches with the same key reuse it.
+ * Launches of one device must be issued on one stream, or the device
+ * synchronises the old stream when it changes. */
 int rt_trace(rt_device *dev, const rt_camera_info *cam, const rt_trace_desc *desc,
              uint64_t *d_rays, void *stream);
 
@@ -218,12 +223,16 @@ int rt_device_synchronize(rt_device *dev);
  * RT_STATS=1: [0] primary wave-iterations, [1] primary lane-segments,
  * [2] secondary wave-iterations, [3] secondary lane-segments, [4] sphere
  * groups tested by primary iterations after culling, [5] secondary groups
- * (exact loop) where some lane passed the distance test.  Returns 1 when
- * enabled, 0 when not (out zeroed), < 0 on error. */
+ * (exact loop) where some lane passed the distance test, [6]/[7] secondary
+ * iterations with < 16 lanes and their lanes, [8] secondary iterations with
+ * no sample left to start, [9]-[15] wave-resident s_memtime cycles in
+ * primary iterations, secondary iterations, the owner fold, block init,
+ * mask load, barrier, and post-barrier setup.  Returns 1 when enabled, 0
+ * when not (out zeroed), < 0 on error. */
 int rt_debug_stats(rt_device *dev, uint64_t out[16], int reset);
 
 /* With RT_WAVETIMES=1: {start, end} s_memrealtime (100 MHz) of every wave of
- * the last trace launch, wave id = (blockIdx.y*gridDim.x + blockIdx.x)*4 + w.
+ * the last trace launch, wave id = block tile * 4 + w (dead tiles are not written).
  * Returns the number of waves copied (0 when disabled), < 0 on error. */
 int64_t rt_debug_wave_times(rt_device *dev, uint64_t *out, uint64_t max_waves);
 
