@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 bash scripts/gpu_check.sh || exit $?
 bash scripts/gpu_pmc.sh c2 > gpurun_out/pmc_c2_stdout.txt 2>&1 || exit $?
-python scripts/pmc_to_json.py gpurun_out pmc_c2_ gpurun_out/c2_pmc.json "C2 1920x1080x256 spp, 1 step" || exit $?
+python scripts/pmc_to_json.py gpurun_out pmc_c2_ gpurun_out/c2_pmc.json "C2: 1920x1080, 256 spp, 64 spheres, 8 bounces, SIMD rules" || exit $?
 bash scripts/gpu_simranks.sh > gpurun_out/simranks.txt 2>&1 || exit $?
 cat gpurun_out/simranks.txt
 for c in c3 c5; do
