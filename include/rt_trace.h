@@ -227,9 +227,12 @@ int rt_device_synchronize(rt_device *dev);
  * iterations with < 16 lanes and their lanes, [8] secondary iterations with
  * no sample left to start, [9]-[15] wave-resident s_memtime cycles in
  * primary iterations, secondary iterations, the owner fold, block init,
- * mask load, barrier, and post-barrier setup.  Returns 1 when enabled, 0
- * when not (out zeroed), < 0 on error. */
-int rt_debug_stats(rt_device *dev, uint64_t out[16], int reset);
+ * mask load, barrier, and post-barrier setup, [16] prefiltered secondary
+ * wave-iterations, [17]/[18] (wave, group) pairs the prefilter flagged, with
+ * and without flags on the sphere a diffuse ray just left, [19]/[20] the same
+ * per sphere pair, [21] lane-level flagged pairs; [22, 32) reserved.
+ * Returns 1 when enabled, 0 when not (out zeroed), < 0 on error. */
+int rt_debug_stats(rt_device *dev, uint64_t out[32], int reset);
 
 /* With RT_WAVETIMES=1: {start, end} s_memrealtime (100 MHz) of every wave of
  * the last trace launch, wave id = block tile * 4 + w (dead tiles are not written).
@@ -246,6 +249,14 @@ int64_t rt_debug_wave_times(rt_device *dev, uint64_t *out, uint64_t max_waves);
  * Arrays may be NULL to query the count. */
 int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p, uint32_t capacity,
                        uint32_t *out_count, uint32_t *out_flags);
+/* The clustered secondary-ray prefilter table rt_scene_upload builds for one
+ * rule set (layout: rt_kernel.h, kClEntryF4 = 3 float4 rows per entry;
+ * cluster-pair entries first).  *out_f4 = float4 rows, *out_cpairs = cluster
+ * pairs (0: the scene uses the per-group prefilter loop).  out may be NULL to
+ * query the size.  Test/inspection hook: the kernel's skip proof is checked
+ * against it on the CPU (tests/test_prefilter_bound.py). */
+int rt_scene_clusters(const rt_scene *scene, uint32_t enable_simd, float *out, uint32_t capacity_f4,
+                      uint32_t *out_f4, uint32_t *out_cpairs);
 const char *rt_last_error(void);
 
 /* ----------------------------------------------- OnInit / OnRender driver */

@@ -112,6 +112,8 @@ SIGNATURES = {
     "rt_debug_wave_times": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
     "rt_scene_prefilter": (c_int, [POINTER(RtScene), c_uint32, c_void_p, c_void_p, c_uint32, POINTER(c_uint32),
                                    POINTER(c_uint32)]),
+    "rt_scene_clusters": (c_int, [POINTER(RtScene), c_uint32, c_void_p, c_uint32, POINTER(c_uint32),
+                                  POINTER(c_uint32)]),
     "rt_last_error": (c_char_p, []),
     "rt_on_init": (c_int, [POINTER(RtInitParams)]),
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
@@ -237,6 +239,19 @@ def scene_prefilter(scene: RtScene, simd: bool = True):
     return r2, r2p, int(fl.value)
 
 
+def scene_clusters(scene: RtScene, simd: bool = True):
+    """The clustered prefilter table rt_scene_upload builds: (table (n, 3, 4)
+    f32 rows, n_cpairs); n_cpairs == 0 means the per-group loop is used."""
+    nf4, ncp = c_uint32(), c_uint32()
+    _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), None, 0, ctypes.byref(nf4), ctypes.byref(ncp)),
+           "rt_scene_clusters")
+    tab = np.zeros((nf4.value, 4), np.float32)
+    if nf4.value:
+        _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), tab.ctypes.data, nf4.value, ctypes.byref(nf4),
+                                       ctypes.byref(ncp)), "rt_scene_clusters")
+    return tab.reshape(-1, 3, 4), int(ncp.value)
+
+
 def rsqrt_table_builtin() -> np.ndarray:
     t = np.zeros(2048, np.float32)
     _check(lib().rt_rsqrt_table_builtin(t.ctypes.data), "rt_rsqrt_table_builtin")
@@ -276,14 +291,15 @@ class Device:
 
     def debug_stats(self, reset: bool = True):
         """RT_STATS=1 scheduling counters (see rt_debug_stats), or None when disabled."""
-        out = np.zeros(16, np.uint64)
+        out = np.zeros(32, np.uint64)
         rc = lib().rt_debug_stats(self.handle, out.ctypes.data, int(reset))
         _check(rc, "rt_debug_stats")
         if rc == 0:
             return None
         keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups",
                 "sec_sparse_iters", "sec_sparse_lanes", "sec_tail_iters", "pri_cycles", "sec_cycles",
-                "fold_cycles", "init_cycles", "cull_cycles", "sync_cycles", "post_cycles"]
+                "fold_cycles", "init_cycles", "cull_cycles", "sync_cycles", "post_cycles", "pf_iters", "pf_groups",
+                "pf_groups_noown", "pf_pairs", "pf_pairs_noown", "pf_lane_pairs"]
         return {k: int(v) for k, v in zip(keys, out) if not k.startswith("_")}
 
     def debug_wave_times(self, max_waves: int = 1 << 22):

@@ -32,6 +32,10 @@ struct rt_device {
     int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
     uint32_t fast_sqrt[2] = {0, 0};  // per rule set: candidate sqrt in sqrt_rn's verified range
+    float4 *d_clusters[2] = {nullptr, nullptr};  // clustered prefilter tables (cluster_table)
+    size_t cap_clusters[2] = {0, 0};             // float4 capacity
+    uint32_t n_cpairs[2] = {0, 0};               // 0: per-group prefilter loop
+    int clusters_env = 1;                        // RT_CLUSTERS=0: per-group prefilter loop (A/B)
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
@@ -103,6 +107,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
     const char *to = getenv("RT_TILE_ORDER");
     if (to && (to[0] == '0' || to[0] == '2')) d->tile_sched = to[0] - '0';  // 2: also for P = 16
+    const char *clu = getenv("RT_CLUSTERS");
+    if (clu && clu[0] == '0') d->clusters_env = 0;
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -111,8 +117,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
         d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
     }
     const char *st = getenv("RT_STATS");
-    if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatCount * sizeof(unsigned long long)) == hipSuccess)
-        (void)hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long));
+    if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatSlots * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(d->d_stats, 0, kStatSlots * sizeof(unsigned long long));
     *out = d;
     return RT_OK;
 }
@@ -124,6 +130,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
     for (int r = 0; r < 2; ++r) {
         (void)hipFree(d->d_groups[r]);
         (void)hipFree(d->d_mats[r]);
+        (void)hipFree(d->d_clusters[r]);
     }
     (void)hipFree(d->d_lut);
     (void)hipFree(d->d_stats);
@@ -226,6 +233,204 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
     return n_ratio > 0 && ratio / n_ratio < 0.5;
 }
 
+// Clustered prefilter table (rt_kernel.h, kClEntryF4 rows per entry) for the
+// secondary-ray sphere loop: the hittable spheres are grouped into about
+// sqrt(n) spatial clusters (deterministic k-means; any membership -- the
+// exact test still runs in the reference's group order).  A cluster c with
+// centre q_c is skipped by a wave when every lane's FMA estimate
+// e_c = |Q|^2 - (Q.D)^2, Q = RN(q_c - O), satisfies e_c >= rc2p_c.  Proof
+// that skipping is exact (u = 2^-24, K = 2^-16, l(p) = the exact squared
+// distance from point p to the ray's line; distance to a line is 1-Lipschitz):
+//  - e_c is within M_c (10.2u + K(1+K)/(1-K)) of l(O + Q) (as for spheres,
+//    plus the 1/|D|^2 factor of l), M_c a bound on |Q|^2 over every secondary
+//    origin; so e_c >= rc2p_c = rho_c^2 + M_c (32u + 1.01K) gives
+//    l(O + Q) >= rho_c^2, and |Q - (q_c - O)| <= u sqrt(M_c) moves the point
+//    by at most that: sqrt(l(q_c)) >= rho_c - u sqrt(M_c);
+//  - member j: sqrt(l(s_j)) >= sqrt(l(q_c)) - |s_j - q_c|, and the
+//    reference's rounded C_j moves s_j by <= u sqrt(M_j) again;
+//  - the reference-rounded dist_j (exact ops on C_j: >= l(O + C_j)) is within
+//    13.3u M_j of its exact value, so l(O + C_j) > sigma_j^2 = r_j^2 + 13.3u M_j
+//    makes dist_j > r_j^2: a miss under both rule sets.
+// Hence rho_c = max_j (|s_j - q_c| + sigma_j + u sqrt(M_j)) + u sqrt(M_c),
+// inflated by 1e-6 relative.  Members of a passing cluster are tested with
+// their own r2p (the per-sphere bound above) and OR'ed into a per-lane mask
+// of flagged sphere pairs; the exact recheck then walks that mask in group
+// order.  Returns the number of cluster-pair entries (0: not used -- more
+// than kClMaxPairs sphere pairs, too few hittable spheres).
+static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, std::vector<float> &tab) {
+    tab.clear();
+    if (2u * n_groups > kClMaxPairs) return 0;
+    struct Sph {
+        uint32_t s;
+        double x, y, z, r, m;
+    };
+    std::vector<Sph> sp;
+    for (uint32_t s = 0; s < 4u * n_groups; ++s) {
+        const uint32_t g = (s / 4u) * 4u * kGroupF4, l = s % 4u;
+        if (!std::isfinite(gv[g + 4u * kRowR2P + l])) continue;  // never flagged (-inf)
+        sp.push_back({s, gv[g + 4u * kRowX + l], gv[g + 4u * kRowY + l], gv[g + 4u * kRowZ + l],
+                      std::sqrt((double)std::max(gv[g + 4u * kRowR2 + l], 0.0f)), 0.0});
+    }
+    const uint32_t n = (uint32_t)sp.size();
+    if (n < 8u) return 0;
+    // reach of every origin (a point on some hittable sphere) from point p, with
+    // the same slack for origin rounding as prefilter_rows
+    auto bound_m = [&](double px, double py, double pz) {
+        double reach = 0.0;
+        for (const Sph &o : sp)
+            reach = std::max(reach, std::sqrt((o.x - px) * (o.x - px) + (o.y - py) * (o.y - py) + (o.z - pz) * (o.z - pz)) + o.r);
+        return (reach * 1.001 + 1e-3) * (reach * 1.001 + 1e-3);
+    };
+    const double u = 0x1p-24, K = 0x1p-16;
+    for (Sph &o : sp) o.m = bound_m(o.x, o.y, o.z);
+    auto sigma = [&](const Sph &o) { return std::sqrt(o.r * o.r + 13.3 * u * o.m) + u * std::sqrt(o.m); };
+    // ~1.25 sqrt(n) clusters: measured on C2 (N = 64) K = 6/8/10/12/16 ->
+    // 112.4k/113.8k/114.6k/114.5k/111.4k Mrays/s
+    uint32_t k = std::max(2u, (uint32_t)std::lround(1.25 * std::sqrt((double)n)));
+    if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob
+    // k-means (f64, fixed LCG restarts) minimising the sum of rho_c^2
+    std::vector<uint32_t> best_lab;
+    double best_cost = INFINITY;
+    uint64_t lcg = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&](uint32_t m) {
+        lcg = lcg * 6364136223846793005ull + 1442695040888963407ull;
+        return (uint32_t)((lcg >> 33) % m);
+    };
+    std::vector<double> cx(k), cy(k), cz(k);
+    std::vector<uint32_t> lab(n);
+    for (int restart = 0; restart < 16; ++restart) {
+        for (uint32_t c = 0; c < k; ++c) {  // k-means++ style seeding (farthest of a few random picks)
+            uint32_t pick = rnd(n);
+            double far = -1.0;
+            for (int t = 0; t < 4 && c > 0; ++t) {
+                const uint32_t cand = rnd(n);
+                double dmin = INFINITY;
+                for (uint32_t q = 0; q < c; ++q)
+                    dmin = std::min(dmin, (sp[cand].x - cx[q]) * (sp[cand].x - cx[q]) + (sp[cand].y - cy[q]) * (sp[cand].y - cy[q]) +
+                                              (sp[cand].z - cz[q]) * (sp[cand].z - cz[q]));
+                if (dmin > far) {
+                    far = dmin;
+                    pick = cand;
+                }
+            }
+            cx[c] = sp[pick].x;
+            cy[c] = sp[pick].y;
+            cz[c] = sp[pick].z;
+        }
+        for (int it = 0; it < 40; ++it) {
+            for (uint32_t i = 0; i < n; ++i) {
+                double dmin = INFINITY;
+                for (uint32_t c = 0; c < k; ++c) {
+                    const double d2 = (sp[i].x - cx[c]) * (sp[i].x - cx[c]) + (sp[i].y - cy[c]) * (sp[i].y - cy[c]) +
+                                      (sp[i].z - cz[c]) * (sp[i].z - cz[c]);
+                    if (d2 < dmin) {
+                        dmin = d2;
+                        lab[i] = c;
+                    }
+                }
+            }
+            std::vector<double> sx(k, 0.0), sy(k, 0.0), sz(k, 0.0), cnt(k, 0.0);
+            for (uint32_t i = 0; i < n; ++i) {
+                sx[lab[i]] += sp[i].x;
+                sy[lab[i]] += sp[i].y;
+                sz[lab[i]] += sp[i].z;
+                cnt[lab[i]] += 1.0;
+            }
+            for (uint32_t c = 0; c < k; ++c)
+                if (cnt[c] > 0.0) {
+                    cx[c] = sx[c] / cnt[c];
+                    cy[c] = sy[c] / cnt[c];
+                    cz[c] = sz[c] / cnt[c];
+                }
+        }
+        std::vector<double> rho(k, 0.0);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t c = lab[i];
+            const double d = std::sqrt((sp[i].x - cx[c]) * (sp[i].x - cx[c]) + (sp[i].y - cy[c]) * (sp[i].y - cy[c]) +
+                                       (sp[i].z - cz[c]) * (sp[i].z - cz[c]));
+            rho[c] = std::max(rho[c], d + sigma(sp[i]));
+        }
+        double cost = 0.0;
+        for (uint32_t c = 0; c < k; ++c) cost += rho[c] * rho[c];
+        if (cost < best_cost) {
+            best_cost = cost;
+            best_lab = lab;
+        }
+    }
+    // final clusters: f32 centres (what the kernel subtracts), exact thresholds
+    struct Cl {
+        float qx, qy, qz, t;
+        std::vector<uint32_t> mem;  // sphere slots, ascending
+    };
+    std::vector<Cl> cl;
+    for (uint32_t c = 0; c < k; ++c) {
+        Cl C;
+        double sx = 0.0, sy = 0.0, sz = 0.0;
+        for (uint32_t i = 0; i < n; ++i)
+            if (best_lab[i] == c) {
+                C.mem.push_back(i);
+                sx += sp[i].x;
+                sy += sp[i].y;
+                sz += sp[i].z;
+            }
+        if (C.mem.empty()) continue;
+        C.qx = (float)(sx / C.mem.size());
+        C.qy = (float)(sy / C.mem.size());
+        C.qz = (float)(sz / C.mem.size());
+        const double qx = C.qx, qy = C.qy, qz = C.qz;
+        double rho = 0.0;
+        for (uint32_t i : C.mem)
+            rho = std::max(rho, std::sqrt((sp[i].x - qx) * (sp[i].x - qx) + (sp[i].y - qy) * (sp[i].y - qy) +
+                                          (sp[i].z - qz) * (sp[i].z - qz)) + sigma(sp[i]));
+        const double mc = bound_m(qx, qy, qz);
+        rho = (rho + u * std::sqrt(mc)) * (1.0 + 1e-6);
+        C.t = std::nextafter((float)(rho * rho + mc * (32.0 * u + 1.01 * K)), INFINITY);
+        for (uint32_t &i : C.mem) i = sp[i].s;
+        cl.push_back(std::move(C));
+    }
+    if (cl.size() & 1u) cl.push_back(Cl{0.0f, 0.0f, 0.0f, -INFINITY, {}});
+    const uint32_t n_cp = (uint32_t)cl.size() / 2u;
+    uint32_t n_mp = 0;
+    for (const Cl &C : cl) n_mp += ((uint32_t)C.mem.size() + 1u) / 2u;
+    tab.assign((size_t)(n_cp + n_mp) * kClEntryF4 * 4u, 0.0f);
+    auto put_u = [&](size_t at, uint32_t v) { memcpy(&tab[at], &v, 4); };
+    auto sphere_xyz = [&](uint32_t s, int axis) {
+        const uint32_t g = (s / 4u) * 4u * kGroupF4, l = s % 4u;
+        return gv[g + 4u * (uint32_t)axis + l];
+    };
+    auto sphere_r2p = [&](uint32_t s) { return gv[(s / 4u) * 4u * kGroupF4 + 4u * kRowR2P + s % 4u]; };
+    uint32_t next = n_cp;
+    for (uint32_t p = 0; p < n_cp; ++p) {
+        float *e = &tab[(size_t)p * kClEntryF4 * 4u];
+        const Cl &A = cl[2u * p], &B = cl[2u * p + 1u];
+        e[0] = A.qx, e[1] = B.qx, e[2] = A.qy, e[3] = B.qy, e[4] = A.qz, e[5] = B.qz, e[6] = A.t, e[7] = B.t;
+        const Cl *two[2] = {&A, &B};
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t cnt = ((uint32_t)two[h]->mem.size() + 1u) / 2u;
+            put_u((size_t)p * kClEntryF4 * 4u + 8u + 2u * h, next);
+            put_u((size_t)p * kClEntryF4 * 4u + 9u + 2u * h, cnt);
+            for (uint32_t q = 0; q < cnt; ++q, ++next) {
+                float *m = &tab[(size_t)next * kClEntryF4 * 4u];
+                const size_t mb = (size_t)next * kClEntryF4 * 4u;
+                for (int w = 0; w < 2; ++w) {
+                    const uint32_t idx = 2u * q + (uint32_t)w;
+                    if (idx < two[h]->mem.size()) {
+                        const uint32_t s = two[h]->mem[idx];
+                        m[0 + w] = sphere_xyz(s, kRowX);
+                        m[2 + w] = sphere_xyz(s, kRowY);
+                        m[4 + w] = sphere_xyz(s, kRowZ);
+                        m[6 + w] = sphere_r2p(s);
+                        put_u(mb + 8u + w, 1u << (s >> 1));
+                    } else {
+                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
+                    }
+                }
+            }
+        }
+    }
+    return n_cp;
+}
+
 // Whether every r^2 the exact test can accept is 0 or in [2^-36, 2^60]: then
 // a passing candidate's r^2 - dist is 0 or >= 2^-60 (it is >= ulp(r^2)/2 when
 // positive), the range where the kernel's short sqrt is verified exact.
@@ -248,6 +453,8 @@ struct PackedSet {
     uint32_t n_groups = 0;
     bool prefilter_pays = false;
     uint32_t fast_sqrt = 0;
+    std::vector<float> clusters;  // cluster_table
+    uint32_t n_cpairs = 0;
 };
 
 static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
@@ -290,6 +497,7 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
     }
     p.prefilter_pays = prefilter_rows(gv, n, rs == 0);
     p.fast_sqrt = sqrt_range_ok(gv, n, rs == 0);
+    p.n_cpairs = cluster_table(gv, n, p.clusters);
     return RT_OK;
 }
 
@@ -306,6 +514,22 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
         d->fast_sqrt[rs] = ps[rs].fast_sqrt;
         const int rc = upload_set(d, rs, ps[rs].groups, ps[rs].mats, ps[rs].n_groups);
         if (rc) return rc;
+        const size_t nf4 = ps[rs].clusters.size() / 4u;
+        d->n_cpairs[rs] = 0;
+        if (nf4 > d->cap_clusters[rs]) {
+            HIP_OK(hipStreamSynchronize(d->stream));
+            (void)hipFree(d->d_clusters[rs]);
+            d->d_clusters[rs] = nullptr;
+            d->cap_clusters[rs] = 0;
+            if (hipMalloc(&d->d_clusters[rs], nf4 * 16u) != hipSuccess)
+                return fail(RT_ENOMEM, "rt_scene_upload: device allocation failed");
+            d->cap_clusters[rs] = nf4;
+        }
+        if (nf4) {
+            HIP_OK(hipMemcpyAsync(d->d_clusters[rs], ps[rs].clusters.data(), nf4 * 16u, hipMemcpyHostToDevice,
+                                  d->stream));
+            d->n_cpairs[rs] = ps[rs].n_cpairs;
+        }
     }
     HIP_OK(hipStreamSynchronize(d->stream));
     d->n_spheres = scene->ScalarSpheres.Count;
@@ -329,6 +553,22 @@ extern "C" int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, f
         const size_t base = (size_t)(s / 4u) * 4u * kGroupF4 + s % 4u;
         if (out_r2) out_r2[s] = p.groups[base + 4u * kRowR2];
         if (out_r2p) out_r2p[s] = p.groups[base + 4u * kRowR2P];
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_scene_clusters(const rt_scene *scene, uint32_t enable_simd, float *out, uint32_t capacity_f4,
+                                 uint32_t *out_f4, uint32_t *out_cpairs) {
+    if (!scene || !out_f4 || !out_cpairs) return fail(RT_EINVAL, "rt_scene_clusters: NULL argument");
+    PackedSet p;
+    const int rc = pack_set(scene, enable_simd ? 0 : 1, p);
+    if (rc) return rc;
+    const uint32_t nf4 = (uint32_t)(p.clusters.size() / 4u);
+    *out_f4 = nf4;
+    *out_cpairs = p.n_cpairs;
+    if (out) {
+        if (capacity_f4 < nf4) return fail(RT_EINVAL, "rt_scene_clusters: capacity %u < %u", capacity_f4, nf4);
+        memcpy(out, p.clusters.data(), (size_t)nf4 * 16u);
     }
     return RT_OK;
 }
@@ -387,6 +627,10 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.sec_threshold = d->sec_threshold;
     a.prefilter = d->prefilter[rs];
     a.fast_sqrt = d->fast_sqrt[rs];
+    if (a.prefilter && d->clusters_env && d->n_cpairs[rs]) {
+        a.clusters = d->d_clusters[rs];
+        a.n_cpairs = d->n_cpairs[rs];
+    }
     a.stats = d->d_stats;
     if (d->want_wave_times) {
         const size_t waves = (size_t)((desc->Width + 7u) / 8u) * ((local_rows + 7u) / 8u) * 4u * 4u;  // >= any shape
@@ -534,14 +778,14 @@ extern "C" int rt_device_synchronize(rt_device *d) {
     return RT_OK;
 }
 
-extern "C" int rt_debug_stats(rt_device *d, uint64_t out[16], int reset) {
+extern "C" int rt_debug_stats(rt_device *d, uint64_t out[32], int reset) {
     if (!d || !out) return fail(RT_EINVAL, "rt_debug_stats: NULL argument");
-    memset(out, 0, 16 * sizeof(uint64_t));
+    memset(out, 0, 32 * sizeof(uint64_t));
     if (!d->d_stats) return 0;
     HIP_OK(hipSetDevice(d->ordinal));
     HIP_OK(hipDeviceSynchronize());
-    HIP_OK(hipMemcpy(out, d->d_stats, kStatCount * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    if (reset) HIP_OK(hipMemset(d->d_stats, 0, kStatCount * sizeof(unsigned long long)));
+    HIP_OK(hipMemcpy(out, d->d_stats, kStatSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (reset) HIP_OK(hipMemset(d->d_stats, 0, kStatSlots * sizeof(unsigned long long)));
     return 1;
 }
 

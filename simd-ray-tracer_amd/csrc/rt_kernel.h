@@ -11,6 +11,14 @@ constexpr uint32_t kRowX = 0, kRowY = 1, kRowZ = 2;  //   centres
 constexpr uint32_t kRowR2P = 3;       //   prefilter thresholds (rows 0-3 = one s_load_dwordx16)
 constexpr uint32_t kRowR2 = 4;        //   r*r
 enum { kFlagAccumZero = 1 };
+// Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
+// kClEntryF4 float4 rows, read through the scalar cache --
+//   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1}
+//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bit0 bit1 0 0}
+// (first/count index member-pair entries; bit = 1 << (sphere slot >> 1), the
+// sphere's pair in group order; padding: threshold -inf, bit 0)
+constexpr uint32_t kClEntryF4 = 3;
+constexpr uint32_t kClMaxPairs = 32;  // one u32 lane mask of flagged sphere pairs (n_groups <= 16)
 
 // HBM layout of an uploaded scene (per rule set):
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
@@ -41,10 +49,14 @@ struct TraceArgs {
     uint32_t *tile_cost;         // optional: per-tile cost (max wave shader cycles), atomicMax'd
     const uint64_t *masks;       // CULL: per wave tile (4*tile + wave) n_words primary group masks
     uint32_t tiles_x;            // block tiles per row (2TW x 2TH pixels each)
+    const float4 *clusters;      // optional: clustered prefilter table (kClEntryF4 rows per entry)
+    uint32_t n_cpairs;           // cluster-pair entries at its start; 0 = per-group prefilter loop
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
-       kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatCount = 16 };
+       kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatPfRounds, kStatPfGroups,
+       kStatPfGroupsNoOwn, kStatPfPairs, kStatPfPairsNoOwn, kStatPfLanePairs, kStatCount = 22 };
+constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 
 // Dynamic LDS per block: rsqrt table + fold table + groups + materials.
 static inline size_t rtk_lds_bytes(uint32_t n_groups) {

@@ -163,6 +163,7 @@ struct Sample {
     float cx, cy, cz;  // output colour
     uint64_t rng;
     uint32_t bounce;
+    uint32_t own;      // RTK_STATS: sphere a diffuse outward bounce left (~0u: none)
 };
 
 // Jittered primary ray (main.cpp:375-385).
@@ -456,11 +457,28 @@ __device__ __forceinline__ void prefilter_group(const Group &G, const RayPk &p, 
 // Group g for a secondary ray through the prefilter: one wave branch per
 // group, and inside it one per flagged pair.  (Measured: +5.5 % on C2 over
 // one exact recheck of both pairs per flagged group.)
+struct PfStats {
+    uint32_t groups, groups_noown, pairs, pairs_noown, lane_pairs;
+};
+
 template <bool SIMD>
 __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
-                                              const RayPk &p, Hit &h) {
+                                              const RayPk &p, Hit &h, uint32_t own = ~0u, PfStats *ps = nullptr) {
     bool f01, f23;
     prefilter_group(G, p, f01, f23);
+    if (ps) {
+        const bool mine = (own >> 2) == g;
+        const uint32_t ol = own & 3u;
+        const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
+        const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
+        const bool n01 = (!(e01.x >= G.r2p[0]) && !(mine && ol == 0u)) | (!(e01.y >= G.r2p[1]) && !(mine && ol == 1u));
+        const bool n23 = (!(e23.x >= G.r2p[2]) && !(mine && ol == 2u)) | (!(e23.y >= G.r2p[3]) && !(mine && ol == 3u));
+        ps->groups += __ballot(f01 | f23) != 0;
+        ps->groups_noown += __ballot(n01 | n23) != 0;
+        ps->pairs += (__ballot(f01) != 0) + (__ballot(f23) != 0);
+        ps->pairs_noown += (__ballot(n01) != 0) + (__ballot(n23) != 0);
+        ps->lane_pairs += __builtin_popcountll(__ballot(f01)) + __builtin_popcountll(__ballot(f23));
+    }
     if (f01 | f23) recheck_pairs<SIMD>(a, lds_groups, G, g, p, h, f01, f23);
 }
 
@@ -480,7 +498,7 @@ __device__ __forceinline__ Group load_group_pf_at(cv4f_t *cg) {
 // through the prefilter; else the exact test.
 template <bool SIMD, bool PF>
 __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray, Hit &h,
-                                                uint32_t *hit_groups) {
+                                                uint32_t *hit_groups, uint32_t own = ~0u, PfStats *ps = nullptr) {
     cv4f_t *gp = (cv4f_t *)a.groups;
     // one group in SGPRs at a time: its s_load (scalar-cache hit) is covered
     // by the other waves on the SIMD -- measured as fast as a ping-pong
@@ -488,8 +506,54 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
     // measured 2 % slower)
     for (uint32_t g = 0; g < a.n_groups; ++g, gp += kGroupF4) {
         const Group G = PF ? load_group_pf_at(gp) : load_group_at(gp);
-        if (PF) test_group_pf<SIMD>(a, lds_groups, G, g, ray, h);
+        if (PF) test_group_pf<SIMD>(a, lds_groups, G, g, ray, h, own, ps);
         else test_group<SIMD>(a, G, g, ray, h, hit_groups);
+    }
+}
+
+// The clustered prefilter (secondary rays; rt_host.cpp cluster_table proves
+// it).  A wave tests the ray against about sqrt(n) cluster bounding volumes,
+// two per packed prefilter, and only the members of a cluster some lane may
+// reach run the per-sphere prefilter; each lane ORs its flagged sphere pairs
+// (bit 2g + half) into `flags`, the wave ORs them into `wave` (SGPRs).  The
+// exact recheck then walks the flagged groups in ascending order -- the
+// reference's order, so the per-class minima, tie rules and sticky inside flags
+// come out as in the full loop.
+__device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
+                                             uint32_t &flags, uint32_t &wave) {
+    for (uint32_t m = first; m < first + count; ++m) {
+        cv4f_t *e = ct + kClEntryF4 * m;
+        const v4f_t r0 = e[0], r1 = e[1];
+        const v4f_t r2 = e[2];
+        const uint32_t b0 = __float_as_uint(r2.x), b1 = __float_as_uint(r2.y);
+        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
+        const bool f0 = !(v.x >= r1.z), f1 = !(v.y >= r1.w);
+        flags |= (f0 ? b0 : 0u) | (f1 ? b1 : 0u);
+        wave |= (__ballot(f0) ? b0 : 0u) | (__ballot(f1) ? b1 : 0u);
+    }
+}
+
+template <bool SIMD>
+__device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray,
+                                                 Hit &h) {
+    cv4f_t *ct = (cv4f_t *)a.clusters;
+    uint32_t flags = 0, wave = 0;
+    for (uint32_t c = 0; c < a.n_cpairs; ++c) {
+        cv4f_t *e = ct + kClEntryF4 * c;
+        const v4f_t r0 = e[0], r1 = e[1];
+        const v4f_t r2 = e[2];
+        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
+        const bool in0 = __ballot(!(v.x >= r1.z)) != 0;
+        const bool in1 = __ballot(!(v.y >= r1.w)) != 0;
+        if (in0) member_pairs(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, flags, wave);
+        if (in1) member_pairs(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, flags, wave);
+    }
+    cv4f_t *gp = (cv4f_t *)a.groups;
+    while (wave) {
+        const uint32_t g = (uint32_t)__builtin_ctz(wave) >> 1;
+        wave &= ~(3u << (2u * g));
+        const bool f01 = (flags >> (2u * g)) & 1u, f23 = (flags >> (2u * g + 1u)) & 1u;
+        recheck_pairs<SIMD>(a, lds_groups, load_group_pf_at(gp + kGroupF4 * g), g, ray, h, f01, f23);
     }
 }
 
@@ -705,8 +769,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
     uint64_t st_cyc_pri = 0, st_cyc_sec = 0, st_cyc_fold = 0, st_cyc_setup = 0;
     uint64_t st_cyc_cull = 0, st_cyc_sync = 0, st_cyc_post = 0;
+    PfStats st_pf = {0, 0, 0, 0, 0};
+    uint32_t st_pf_rounds = 0;
     Sample p;
     p.bounce = 0;
+    p.own = ~0u;
     p.cx = p.cy = p.cz = 0.0f;
 
     // Empty tile: no sphere group passes the tile's (conservative) cone test,
@@ -798,8 +865,13 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         // needs |D|^2 within 2^-16 of 1 on every lane (else exact).
                         const float u2 = __builtin_fmaf(p.rx.y, p.rx.y, __builtin_fmaf(p.ry.y, p.ry.y, p.rz.y * p.rz.y));
                         const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
-                        if (SRC == kSrcSmem && pf) {
-                            all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr);
+                        if (SRC == kSrcSmem && pf && a.n_cpairs) {
+                            if (kStats && a.stats) st_pf_rounds += 1;
+                            clustered_groups<SIMD>(a, lds_groups, ray, h);
+                        } else if (SRC == kSrcSmem && pf) {
+                            if (kStats && a.stats) st_pf_rounds += 1;
+                            all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr, p.own,
+                                                        kStats && a.stats ? &st_pf : nullptr);
                         } else if (SRC == kSrcSmem) {
                             all_groups_smem<SIMD, false>(a, lds_groups, ray, h, kStats && a.stats ? &st_sec_hit : nullptr);
                         } else {
@@ -853,6 +925,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         const float4 cs = lds_mats[2u * sidx + 0u];
                         const float4 ei = lds_mats[2u * sidx + 1u];
                         shade(lut, cs, ei, hx, hy, hz, inside, p);
+                        if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
                         p.bounce += 1;
                         done = p.bounce == a.max_bounce;
                     }
@@ -953,6 +1026,12 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatCullCycles, (unsigned long long)st_cyc_cull);
         atomicAdd(a.stats + kStatSyncCycles, (unsigned long long)st_cyc_sync);
         atomicAdd(a.stats + kStatPostCycles, (unsigned long long)st_cyc_post);
+        atomicAdd(a.stats + kStatPfRounds, (unsigned long long)st_pf_rounds);
+        atomicAdd(a.stats + kStatPfGroups, (unsigned long long)st_pf.groups);
+        atomicAdd(a.stats + kStatPfGroupsNoOwn, (unsigned long long)st_pf.groups_noown);
+        atomicAdd(a.stats + kStatPfPairs, (unsigned long long)st_pf.pairs);
+        atomicAdd(a.stats + kStatPfPairsNoOwn, (unsigned long long)st_pf.pairs_noown);
+        atomicAdd(a.stats + kStatPfLanePairs, (unsigned long long)st_pf.lane_pairs);
     }
 }
 

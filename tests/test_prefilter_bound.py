@@ -111,3 +111,74 @@ def test_short_sqrt_flag_follows_the_radius_range(rt):
     sp[3, 4] = np.float32(2e-6)  # r^2 = 4e-12 < 2^-36: outside the verified range
     tiny = rt.scene_from_spheres(sp)
     assert not rt.scene_prefilter(tiny, True)[2] & 2 and not rt.scene_prefilter(tiny, False)[2] & 2
+
+
+@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 37), (1, 16), (0, None)])
+@pytest.mark.parametrize("simd", [True, False])
+def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
+    """The clustered loop (rt_kernel.hip clustered_groups) skips every member
+    of a cluster when e_c >= rc2p_c on all lanes; the members of a tested
+    cluster are flagged by their own r2p.  Every exact hit must survive both
+    levels, and every hittable sphere must be a member of exactly one cluster."""
+    scene = rt.scene_builtin(idx)
+    if n_spheres:
+        scene = rt.scene_prefix(scene, n_spheres)
+    tab, ncp = rt.scene_clusters(scene, simd)
+    r2, r2p, _ = rt.scene_prefilter(scene, simd)
+    if ncp == 0:
+        pytest.skip("scene uses the per-group prefilter loop")
+    sp, groups, _ = rt.scene_arrays(scene)
+    if simd:
+        cx_, cy_, cz_ = groups[:, 0:4].ravel(), groups[:, 4:8].ravel(), groups[:, 8:12].ravel()
+        radius = groups[:, 12:16].ravel()
+    else:
+        pad = (-len(sp)) % 4
+        cx_, cy_, cz_ = (np.concatenate([sp[:, k], np.zeros(pad, F)]) for k in range(3))
+        radius = np.concatenate([sp[:, 4], np.zeros(pad, F)])
+    centres = np.stack([cx_, cy_, cz_], 1).astype(F)
+    live = np.isfinite(r2p)
+    # decode the table: clusters -> member spheres (by centre and r2p) and pair bits
+    members = []
+    for c in range(ncp):
+        q = tab[c]
+        u = q[2].view(np.uint32)
+        for h in range(2):
+            first, count = int(u[2 * h]), int(u[2 * h + 1])
+            ms = []
+            for m in range(first, first + count):
+                e = tab[m]
+                bits = e[2].view(np.uint32)
+                for w in range(2):
+                    if np.isneginf(e[1][2 + w]):
+                        assert bits[w] == 0
+                        continue
+                    x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
+                    s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
+                                       (r2p == t) & live)
+                    assert len(s) >= 1
+                    s = [k for k in s if bits[w] == (1 << (k >> 1))]
+                    assert len(s) >= 1, "member pair bit is not its sphere's pair in group order"
+                    ms.append(s[0])
+            members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
+                            np.float32(q[1][2 + h]), ms))
+    covered = sorted(s for m in members for s in m[4])
+    assert covered == sorted(np.flatnonzero(live)), "every hittable sphere is in exactly one cluster"
+    rng = np.random.default_rng(11 + idx)
+    o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), 4000)
+    dx, dy, dz = d[:, None, 0], d[:, None, 1], d[:, None, 2]
+    cx = centres[None, :, 0] - o[:, None, 0]
+    cy = centres[None, :, 1] - o[:, None, 1]
+    cz = centres[None, :, 2] - o[:, None, 2]
+    dist = exact_dist(cx, cy, cz, dx, dy, dz)
+    hit = ((dist < r2) if simd else ~(dist > r2)) & live[None, :]
+    assert hit.sum() > 0
+    skipped_any = 0
+    for qx, qy, qz, t, ms in members:
+        if np.isneginf(t):
+            continue
+        ex = prefilter((qx - o[:, 0])[:, None], (qy - o[:, 1])[:, None], (qz - o[:, 2])[:, None],
+                       d[:, 0:1], d[:, 1:2], d[:, 2:3])[:, 0]
+        skip = ~(ex < t)
+        skipped_any += int(skip.sum())
+        assert not np.any(hit[skip][:, ms]), "a skipped cluster holds an exact hit"
+    assert skipped_any > 0  # the level does cull
