@@ -110,6 +110,7 @@ SIGNATURES = {
     "rt_device_synchronize": (c_int, [c_void_p]),
     "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "rt_debug_wave_times": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
+    "rt_debug_masks": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
     "rt_scene_prefilter": (c_int, [POINTER(RtScene), c_uint32, c_void_p, c_void_p, c_uint32, POINTER(c_uint32),
                                    POINTER(c_uint32)]),
     "rt_scene_clusters": (c_int, [POINTER(RtScene), c_uint32, c_void_p, c_uint32, POINTER(c_uint32),
@@ -308,6 +309,13 @@ class Device:
         n = int(lib().rt_debug_wave_times(self.handle, out.ctypes.data, max_waves))
         _check(n, "rt_debug_wave_times")
         return out[: 2 * n].reshape(-1, 2) if n else None
+
+    def debug_masks(self, max_words: int = 1 << 24):
+        """Primary group masks of the last cull pass (see rt_debug_masks), or None."""
+        out = np.zeros(max_words, np.uint64)
+        n = int(lib().rt_debug_masks(self.handle, out.ctypes.data, max_words))
+        _check(n, "rt_debug_masks")
+        return out[:n].copy() if n else None
 
     def synchronize(self) -> None:
         _check(lib().rt_device_synchronize(self.handle), "rt_device_synchronize")

@@ -35,7 +35,13 @@ struct rt_device {
     float4 *d_clusters[2] = {nullptr, nullptr};  // clustered prefilter tables (cluster_table)
     size_t cap_clusters[2] = {0, 0};             // float4 capacity
     uint32_t n_cpairs[2] = {0, 0};               // 0: per-group prefilter loop
-    int clusters_env = 1;                        // RT_CLUSTERS=0: per-group prefilter loop (A/B)
+    uint32_t cl_words[2] = {0, 0};
+    // RT_CLUSTERS=0: per-group prefilter loop only; 2: clustered loop up to
+    // kClMaxGroups groups; default 1: up to kClAutoGroups (measured on C2
+    // geometry: clusters win 13-15 % at 16/24/32 groups and lose 18 % at 64,
+    // where the denser 256-sphere scene leaves the waves' secondary rays too
+    // incoherent for a wave-wide cluster skip)
+    int clusters_env = 1;
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
@@ -45,6 +51,7 @@ struct rt_device {
     unsigned long long *d_cull_counters = nullptr;  // 2 x 64 striped counters of the cull pass
     uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
     size_t tile_cap = 0, mask_cap = 0;
+    size_t mask_words = 0;  // words the last cull pass wrote (rt_debug_masks)
     // the launch (camera, scene, geometry) the masks / live list / order were made for
     std::vector<uint32_t> tile_key;
     bool tile_order_valid = false;
@@ -108,7 +115,7 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     const char *to = getenv("RT_TILE_ORDER");
     if (to && (to[0] == '0' || to[0] == '2')) d->tile_sched = to[0] - '0';  // 2: also for P = 16
     const char *clu = getenv("RT_CLUSTERS");
-    if (clu && clu[0] == '0') d->clusters_env = 0;
+    if (clu && (clu[0] == '0' || clu[0] == '2')) d->clusters_env = clu[0] - '0';
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -253,13 +260,16 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
 //    makes dist_j > r_j^2: a miss under both rule sets.
 // Hence rho_c = max_j (|s_j - q_c| + sigma_j + u sqrt(M_j)) + u sqrt(M_c),
 // inflated by 1e-6 relative.  Members of a passing cluster are tested with
-// their own r2p (the per-sphere bound above) and OR'ed into a per-lane mask
-// of flagged sphere pairs; the exact recheck then walks that mask in group
-// order.  Returns the number of cluster-pair entries (0: not used -- more
-// than kClMaxPairs sphere pairs, too few hittable spheres).
-static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, std::vector<float> &tab) {
+// their own r2p (the per-sphere bound above); a sphere pair some lane may
+// hit sets its bit in the wave's pair mask, and the exact recheck walks that
+// mask in group order.  Returns the number of cluster-pair entries (0: not
+// used -- more than kClMaxGroups groups, too few hittable spheres); *words =
+// u64 words of the pair mask.
+static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, std::vector<float> &tab,
+                              uint32_t *words) {
     tab.clear();
-    if (2u * n_groups > kClMaxPairs) return 0;
+    *words = n_groups <= 32u ? 1u : 2u;
+    if (n_groups > kClMaxGroups) return 0;
     struct Sph {
         uint32_t s;
         double x, y, z, r, m;
@@ -420,9 +430,10 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
                         m[2 + w] = sphere_xyz(s, kRowY);
                         m[4 + w] = sphere_xyz(s, kRowZ);
                         m[6 + w] = sphere_r2p(s);
-                        put_u(mb + 8u + w, 1u << (s >> 1));
+                        put_u(mb + 8u + w, s >> 1);
                     } else {
-                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
+                        m[6 + w] = -INFINITY;  // padding member: never flagged
+                        put_u(mb + 8u + w, 0xFFFFFFFFu);
                     }
                 }
             }
@@ -454,7 +465,7 @@ struct PackedSet {
     bool prefilter_pays = false;
     uint32_t fast_sqrt = 0;
     std::vector<float> clusters;  // cluster_table
-    uint32_t n_cpairs = 0;
+    uint32_t n_cpairs = 0, cl_words = 0;
 };
 
 static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
@@ -497,7 +508,7 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
     }
     p.prefilter_pays = prefilter_rows(gv, n, rs == 0);
     p.fast_sqrt = sqrt_range_ok(gv, n, rs == 0);
-    p.n_cpairs = cluster_table(gv, n, p.clusters);
+    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words);
     return RT_OK;
 }
 
@@ -529,6 +540,7 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
             HIP_OK(hipMemcpyAsync(d->d_clusters[rs], ps[rs].clusters.data(), nf4 * 16u, hipMemcpyHostToDevice,
                                   d->stream));
             d->n_cpairs[rs] = ps[rs].n_cpairs;
+            d->cl_words[rs] = ps[rs].cl_words;
         }
     }
     HIP_OK(hipStreamSynchronize(d->stream));
@@ -627,9 +639,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.sec_threshold = d->sec_threshold;
     a.prefilter = d->prefilter[rs];
     a.fast_sqrt = d->fast_sqrt[rs];
-    if (a.prefilter && d->clusters_env && d->n_cpairs[rs]) {
+    if (a.prefilter && d->n_cpairs[rs] &&
+        (d->clusters_env == 2 || (d->clusters_env == 1 && d->n_groups[rs] <= kClAutoGroups))) {
         a.clusters = d->d_clusters[rs];
         a.n_cpairs = d->n_cpairs[rs];
+        a.cl_words = d->cl_words[rs];
     }
     a.stats = d->d_stats;
     if (d->want_wave_times) {
@@ -720,6 +734,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         d->tile_key = key;
         if (cull) {
             a.masks = d->d_masks;
+            d->mask_words = mask_words;
             if (rtk_launch_cull(&a, lpp, d->d_tile_live, d->d_tile_cost, d->d_cull_counters, empty_capable ? 1 : 0, s) !=
                     0 ||
                 rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
@@ -787,6 +802,16 @@ extern "C" int rt_debug_stats(rt_device *d, uint64_t out[32], int reset) {
     HIP_OK(hipMemcpy(out, d->d_stats, kStatSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (reset) HIP_OK(hipMemset(d->d_stats, 0, kStatSlots * sizeof(unsigned long long)));
     return 1;
+}
+
+extern "C" int64_t rt_debug_masks(rt_device *d, uint64_t *out, uint64_t max_words) {
+    if (!d || !out) return fail(RT_EINVAL, "rt_debug_masks: NULL argument");
+    if (!d->d_masks || d->tile_key.empty() || !d->mask_words) return 0;
+    const uint64_t n = max_words < d->mask_words ? max_words : d->mask_words;
+    HIP_OK(hipSetDevice(d->ordinal));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(out, d->d_masks, n * 8u, hipMemcpyDeviceToHost));
+    return (int64_t)n;
 }
 
 extern "C" int64_t rt_debug_wave_times(rt_device *d, uint64_t *out, uint64_t max_waves) {

@@ -14,11 +14,14 @@ enum { kFlagAccumZero = 1 };
 // Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
 // kClEntryF4 float4 rows, read through the scalar cache --
 //   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1}
-//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bit0 bit1 0 0}
-// (first/count index member-pair entries; bit = 1 << (sphere slot >> 1), the
-// sphere's pair in group order; padding: threshold -inf, bit 0)
+//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {pair0 pair1 0 0}
+// (first/count index member-pair entries; pair = sphere slot >> 1, the
+// sphere's pair in group order, the bit it sets in the wave's pair mask;
+// padding: threshold -inf, pair 0xFFFFFFFF).  The wave mask is kept in
+// SGPRs, cl_words u64 words of it (1: n_groups <= 32, 2: n_groups <= 64).
 constexpr uint32_t kClEntryF4 = 3;
-constexpr uint32_t kClMaxPairs = 32;  // one u32 lane mask of flagged sphere pairs (n_groups <= 16)
+constexpr uint32_t kClMaxGroups = 64;   // table built up to this many groups
+constexpr uint32_t kClAutoGroups = 32;  // used by default up to this many (rt_host.cpp clusters_env)
 
 // HBM layout of an uploaded scene (per rule set):
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
@@ -51,6 +54,7 @@ struct TraceArgs {
     uint32_t tiles_x;            // block tiles per row (2TW x 2TH pixels each)
     const float4 *clusters;      // optional: clustered prefilter table (kClEntryF4 rows per entry)
     uint32_t n_cpairs;           // cluster-pair entries at its start; 0 = per-group prefilter loop
+    uint32_t cl_words;           // u64 words of the clustered loop's pair mask (1 or 2)
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,

@@ -514,30 +514,41 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // The clustered prefilter (secondary rays; rt_host.cpp cluster_table proves
 // it).  A wave tests the ray against about sqrt(n) cluster bounding volumes,
 // two per packed prefilter, and only the members of a cluster some lane may
-// reach run the per-sphere prefilter; each lane ORs its flagged sphere pairs
-// (bit 2g + half) into `flags`, the wave ORs them into `wave` (SGPRs).  The
+// reach run the per-sphere prefilter; a sphere pair some lane may hit sets
+// bit (slot >> 1) of the wave's pair mask (W u64 words, SGPRs only).  The
 // exact recheck then walks the flagged groups in ascending order -- the
 // reference's order, so the per-class minima, tie rules and sticky inside flags
-// come out as in the full loop.
+// come out as in the full loop.  The recheck runs on every lane: a lane whose
+// own estimate cleared the pair has a proven miss there, which its exact test
+// reproduces, so no per-lane flags are needed.
+template <int W>
+__device__ __forceinline__ void set_pair(uint64_t (&wave)[2], bool any, uint32_t q) {
+    const uint64_t bit = any ? 1ull << (q & 63u) : 0ull;  // padding (q = ~0) never has any
+    if (W == 1) wave[0] |= bit;
+    else {
+        wave[0] |= q < 64u ? bit : 0ull;
+        wave[1] |= q < 64u ? 0ull : bit;
+    }
+}
+
+template <int W>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
-                                             uint32_t &flags, uint32_t &wave) {
+                                             uint64_t (&wave)[2]) {
     for (uint32_t m = first; m < first + count; ++m) {
         cv4f_t *e = ct + kClEntryF4 * m;
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2];
-        const uint32_t b0 = __float_as_uint(r2.x), b1 = __float_as_uint(r2.y);
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
-        const bool f0 = !(v.x >= r1.z), f1 = !(v.y >= r1.w);
-        flags |= (f0 ? b0 : 0u) | (f1 ? b1 : 0u);
-        wave |= (__ballot(f0) ? b0 : 0u) | (__ballot(f1) ? b1 : 0u);
+        set_pair<W>(wave, __ballot(!(v.x >= r1.z)) != 0, __float_as_uint(r2.x));
+        set_pair<W>(wave, __ballot(!(v.y >= r1.w)) != 0, __float_as_uint(r2.y));
     }
 }
 
-template <bool SIMD>
+template <bool SIMD, int W>
 __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray,
                                                  Hit &h) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
-    uint32_t flags = 0, wave = 0;
+    uint64_t wave[2] = {0ull, 0ull};
     for (uint32_t c = 0; c < a.n_cpairs; ++c) {
         cv4f_t *e = ct + kClEntryF4 * c;
         const v4f_t r0 = e[0], r1 = e[1];
@@ -545,15 +556,20 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
         const bool in0 = __ballot(!(v.x >= r1.z)) != 0;
         const bool in1 = __ballot(!(v.y >= r1.w)) != 0;
-        if (in0) member_pairs(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, flags, wave);
-        if (in1) member_pairs(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, flags, wave);
+        if (in0) member_pairs<W>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave);
+        if (in1) member_pairs<W>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave);
     }
     cv4f_t *gp = (cv4f_t *)a.groups;
-    while (wave) {
-        const uint32_t g = (uint32_t)__builtin_ctz(wave) >> 1;
-        wave &= ~(3u << (2u * g));
-        const bool f01 = (flags >> (2u * g)) & 1u, f23 = (flags >> (2u * g + 1u)) & 1u;
-        recheck_pairs<SIMD>(a, lds_groups, load_group_pf_at(gp + kGroupF4 * g), g, ray, h, f01, f23);
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        uint64_t m = wave[w];
+        while (m) {
+            const uint32_t q = (uint32_t)__builtin_ctzll(m) & ~1u;  // first pair of the lowest flagged group
+            const uint32_t g = 32u * (uint32_t)w + (q >> 1);
+            const bool f01 = (m >> q) & 1u, f23 = (m >> (q + 1u)) & 1u;
+            m &= ~(3ull << q);
+            recheck_pairs<SIMD>(a, lds_groups, load_group_pf_at(gp + kGroupF4 * g), g, ray, h, f01, f23);
+        }
     }
 }
 
@@ -850,9 +866,12 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     const RayPk ray = {p.rx, p.ry, p.rz};
                     if (CULL && !do_sec) {
                         for (uint32_t w = 0; w < n_words; ++w) {
-                            uint64_t m = __builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]) |
-                                         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32))
-                                          << 32);
+                            // (readfirstlane returns int: widen each half as u32, or
+                            // bit 31 would sign-extend into groups 32..63)
+                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]);
+                            const uint32_t hi =
+                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32));
+                            uint64_t m = (uint64_t)lo | ((uint64_t)hi << 32);
                             if (kStats && a.stats) st_groups += __builtin_popcountll(m);
                             while (m) {
                                 const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
@@ -867,7 +886,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
                         if (SRC == kSrcSmem && pf && a.n_cpairs) {
                             if (kStats && a.stats) st_pf_rounds += 1;
-                            clustered_groups<SIMD>(a, lds_groups, ray, h);
+                            if (a.cl_words == 1u) clustered_groups<SIMD, 1>(a, lds_groups, ray, h);
+                            else clustered_groups<SIMD, 2>(a, lds_groups, ray, h);
                         } else if (SRC == kSrcSmem && pf) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr, p.own,

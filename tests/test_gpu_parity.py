@@ -60,7 +60,8 @@ CONFIGS = [
     (1, 4, 256, 256, 1, 1, False),
     (1, 64, 128, 96, 8, 8, True),      # C2/C3 geometry, scaled image
     (1, 64, 128, 96, 8, 8, False),
-    (1, 256, 64, 64, 2, 16, True),     # C5 geometry, scaled image
+    (1, 256, 64, 64, 2, 16, True),     # C5 geometry, scaled image (64 groups: per-group prefilter loop)
+    (1, 100, 48, 40, 3, 8, False),     # 25 groups: clustered prefilter under the scalar rules
     (0, None, 96, 64, 4, 5, True),     # RGB Glass: dielectric + sticky inside flag
     (0, None, 96, 64, 4, 5, False),
     (2, None, 80, 48, 2, 5, True),     # RTWeekend: sky term, glass, 482 spheres
@@ -68,6 +69,12 @@ CONFIGS = [
     (1, 13, 37, 23, 3, 6, True),       # ragged N (padding lanes) and image not a tile multiple
     (1, 13, 37, 23, 3, 6, False),
     (1, 1, 1, 1, 4, 3, True),          # single pixel, single sphere
+    # 32 / 50 groups: primary masks with bit 31 set (a sign-extended mask word once
+    # tested groups past the scene: history-dependent misses at these sizes)
+    (1, 128, 16, 16, 1, 1, True),
+    (1, 128, 16, 8, 1, 1, True),
+    (1, 200, 40, 32, 3, 8, True),
+    (1, 200, 40, 32, 3, 8, False),
 ]
 
 
@@ -201,7 +208,7 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
 # Kernel variants selected at device creation (rt_host.cpp reads the env):
 # prefilter forced on/off, brute-force primaries, 1/2 lanes per pixel.  Every
 # variant must give the same bits as the oracle.
-VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CULL": "0"},
+VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"}, {"RT_CULL": "0"},
                 {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"}, {"RT_SEC_THRESHOLD": "1"}]
 
 
@@ -211,7 +218,9 @@ def test_kernel_variants_match_oracle(rt, orc, torch_cuda, monkeypatch, env):
         monkeypatch.setenv(k, v)
     dev = rt.Device(0)
     try:
-        for scene_idx, n, W, H, spp, B in [(1, 64, 64, 48, 6, 8), (0, None, 48, 32, 4, 5), (2, None, 40, 24, 2, 5)]:
+        # (1, 200): 50 groups, the two-word cluster mask under RT_CLUSTERS=2
+        for scene_idx, n, W, H, spp, B in [(1, 64, 64, 48, 6, 8), (1, 200, 40, 32, 3, 8), (0, None, 48, 32, 4, 5),
+                                           (2, None, 40, 24, 2, 5)]:
             for simd in (True, False):
                 s, o = _scenes(rt, orc, scene_idx, n)
                 cam = rt.camera_setup(s, W, H)

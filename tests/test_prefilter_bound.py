@@ -113,7 +113,7 @@ def test_short_sqrt_flag_follows_the_radius_range(rt):
     assert not rt.scene_prefilter(tiny, True)[2] & 2 and not rt.scene_prefilter(tiny, False)[2] & 2
 
 
-@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 37), (1, 16), (0, None)])
+@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 37), (1, 16), (1, 100), (1, 256), (0, None)])
 @pytest.mark.parametrize("simd", [True, False])
 def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     """The clustered loop (rt_kernel.hip clustered_groups) skips every member
@@ -137,7 +137,7 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
         radius = np.concatenate([sp[:, 4], np.zeros(pad, F)])
     centres = np.stack([cx_, cy_, cz_], 1).astype(F)
     live = np.isfinite(r2p)
-    # decode the table: clusters -> member spheres (by centre and r2p) and pair bits
+    # decode the table: clusters -> member spheres (by centre and r2p) and pair indices
     members = []
     for c in range(ncp):
         q = tab[c]
@@ -147,17 +147,17 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
             ms = []
             for m in range(first, first + count):
                 e = tab[m]
-                bits = e[2].view(np.uint32)
+                pair = e[2].view(np.uint32)
                 for w in range(2):
                     if np.isneginf(e[1][2 + w]):
-                        assert bits[w] == 0
+                        assert pair[w] == 0xFFFFFFFF
                         continue
                     x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
                     s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
                                        (r2p == t) & live)
                     assert len(s) >= 1
-                    s = [k for k in s if bits[w] == (1 << (k >> 1))]
-                    assert len(s) >= 1, "member pair bit is not its sphere's pair in group order"
+                    s = [k for k in s if pair[w] == k >> 1]
+                    assert len(s) >= 1, "member pair index is not its sphere's pair in group order"
                     ms.append(s[0])
             members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
                             np.float32(q[1][2 + h]), ms))
