@@ -1,6 +1,6 @@
 """Diagnostic (CPU): which spheres can a pixel's jittered primary rays hit (f64
 line test over a jitter grid), and are their groups in the cull mask of the
-pixel's wave tile (numpy restatement in masks.py)?
+pixel's wave tile (numpy restatement in tests/cull_ref.py)?
 Usage: python scripts/diag/pixel_hits.py N W H P x y"""
 import pathlib
 import sys
@@ -11,16 +11,15 @@ ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 import __graft_entry__ as g  # noqa: E402
 
+sys.path.insert(0, str(ROOT / "tests"))
+from cull_ref import SHAPE, np_masks  # noqa: E402
+
 rt = g.load_package()
-src = (ROOT / "scripts/diag/masks.py").read_text().split("for n, W, H, P in")[0].replace("import torch", "")
-ns = {"__file__": str(ROOT / "scripts/diag/masks.py")}
-exec(src, ns)
-SHAPE = ns["SHAPE"]
 
 n, W, H, P, x, y = (int(v) for v in sys.argv[1:7])
 s = rt.scene_prefix(rt.scene_builtin(1), n)
 cam = rt.camera_setup(s, W, H)
-m = ns["np_masks"](s, cam, W, H, P)
+m = np_masks(rt, s, cam, W, H, P)
 _, groups, _ = rt.scene_arrays(s)
 c = np.stack([groups[:, 0:4].ravel(), groups[:, 4:8].ravel(), groups[:, 8:12].ravel()], 1).astype(np.float64)
 r = groups[:, 12:16].ravel().astype(np.float64)

@@ -331,3 +331,25 @@ def test_camera_change_recomputes_the_cull_pass(rt, orc, torch_cuda, gdev):
         g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5)
         r = orc.render(o, orc.camera(o, W, H, distance=dist, x_angle=ang), W, H, frames=2, max_bounce=5)
         assert_same(*g, *r)
+
+
+@pytest.mark.parametrize("idx,n,W,H,P", [(1, 64, 96, 64, 4), (1, 128, 16, 16, 1), (1, 200, 40, 32, 2),
+                                         (1, 256, 64, 48, 8), (0, None, 48, 32, 16)])
+def test_cull_masks_equal_cpu_restatement(rt, torch_cuda, monkeypatch, idx, n, W, H, P):
+    """The cull pass's primary group masks (rt_debug_masks) equal the numpy f64
+    restatement (tests/cull_ref.py) word for word; tests/test_cull_bound.py
+    checks that restatement keeps every group a pixel's rays can reach."""
+    from cull_ref import np_masks
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", str(P))
+    s = rt.scene_builtin(idx)
+    if n:
+        s = rt.scene_prefix(s, n)
+    cam = rt.camera_setup(s, W, H)
+    dev = rt.Device(0)
+    try:
+        gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=1, bounces=1)
+        got = dev.debug_masks()
+    finally:
+        dev.close()
+    ref = np_masks(rt, s, cam, W, H, P)
+    assert got is not None and np.array_equal(got, ref), np.flatnonzero(got != ref)[:8]
