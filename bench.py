@@ -54,7 +54,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", choices=sorted(CONFIGS), default="c2", help="BASELINE.json workload preset")
     p.add_argument("--width", type=int)
     p.add_argument("--height", type=int)

@@ -3,7 +3,7 @@
 # the assembled frame bit-for-bit against a one-rank render.
 set -o pipefail
 mkdir -p gpurun_out
-for n in 2 3; do
+for n in 2 3 8; do
   BENCH_BACKEND=gloo BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
     --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --steps 3 --warmup 1 --verify \
     --width 640 --height 360 --spp 32 > gpurun_out/mr$n.json 2> gpurun_out/mr$n.err || { tail -20 gpurun_out/mr$n.err; exit 1; }

@@ -113,7 +113,7 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     const char *pf = getenv("RT_PREFILTER");  // secondary-ray prefilter: 0 off, 1 on, unset = per-scene auto
     if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
     const char *to = getenv("RT_TILE_ORDER");
-    if (to && (to[0] == '0' || to[0] == '2')) d->tile_sched = to[0] - '0';  // 2: also for P = 16
+    if (to && to[0] == '0') d->tile_sched = 0;
     const char *clu = getenv("RT_CLUSTERS");
     if (clu && (clu[0] == '0' || clu[0] == '2')) d->clusters_env = clu[0] - '0';
     const char *wt = getenv("RT_WAVETIMES");
@@ -659,14 +659,16 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     // Lanes per pixel (measured on MI355X at 1/2/4/8-way band splits of C2,
-    // bench.py --sim-ranks): 4 while the band has >= ~3k pixels per CU, else 8
-    // (more lanes per pixel shortens the per-lane sample chains that form the
-    // launch tail; 16 lost to 8 once tiles run heaviest-first); never more
-    // lanes than frames.
+    // bench.py --sim-ranks, heaviest-first order at every P): 4 while the band
+    // has >= 6k pixels per CU, 8 down to 1.5k, else 16 (more lanes per pixel
+    // shorten the per-lane sample chains that form the launch tail; C2 rank
+    // shares: 1 GPU P=4 6.21 ms (P=8 6.29, P=16 6.62); 2 ranks P=8 3.26 ms
+    // (P=4 3.35); 4 ranks P=8 = P=16 1.81 ms; 8 ranks P=16 1.02 ms (P=8
+    // 1.47)); never more lanes than frames.
     int lpp = d->lanes_per_pixel;
     if (lpp == 0) {
         const uint64_t pixels = (uint64_t)desc->Width * local_rows;
-        lpp = pixels >= (uint64_t)d->cu_count * 3072u ? 4 : 8;
+        lpp = pixels >= (uint64_t)d->cu_count * 6144u ? 4 : pixels >= (uint64_t)d->cu_count * 1536u ? 8 : 16;
         while (lpp > 1 && (uint32_t)lpp / 2u >= desc->Frames) lpp /= 2;
     }
     // Tile scheduling.  Block tiles (2TW x 2TH pixels) are traced in the order
@@ -681,7 +683,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     const bool cull = d->cull != 0;
     const bool empty_capable = cull && !d->use_sky && desc->MaxBounce != 0;
-    const bool sched = d->tile_sched == 2 || (d->tile_sched && lpp <= 8);
+    const bool sched = d->tile_sched != 0;
     a.tiles_x = rtk_tiles_x(desc->Width, lpp);
     std::vector<uint32_t> key = {desc->Width, desc->Height, local_rows, band_rows, band_count, desc->BandIndex,
                                  (uint32_t)lpp, (uint32_t)rs, (uint32_t)cull, (uint32_t)empty_capable, (uint32_t)sched,
