@@ -293,6 +293,18 @@ int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
 int rt_on_render_wait(void);
 int rt_on_shutdown(void);
 
+/* ----------------------------------------------------------- output path */
+
+/* The RGBA8 frame (RT_FORMAT_R8G8B8A8_U32, host memory) written as a binary
+ * PPM (P6, RGB) or an 8-bit RGBA PNG (stored deflate blocks), in place of
+ * the reference's WebGL texture upload of Image.Data (wasm/wasm.cpp:216-218).
+ * RT_IMAGE_FLIP_Y writes image row Height-1 first: the texture's row 0 is the
+ * bottom of the window, so that is the on-screen orientation.
+ * Returns RT_OK, RT_EINVAL (bad image / format / path) or RT_EIO. */
+#define RT_IMAGE_FLIP_Y 1u
+int rt_image_write_ppm(const rt_image *image, const char *path, uint32_t flags);
+int rt_image_write_png(const rt_image *image, const char *path, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,8 +24,8 @@ for _ in range(2):
     dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
               frames=S, max_bounce=B, accum_zero=True, band_rows=8, band_count=G, band_index=0)
 torch.cuda.synchronize()
-wt = dev.debug_wave_times().astype(np.int64)
-wt = wt[wt[:, 1] > 0]
+wt_all = dev.debug_wave_times().astype(np.int64)
+wt = wt_all[wt_all[:, 1] > 0]
 t0 = wt[:, 0].min()
 st, en = (wt[:, 0] - t0) / 100.0, (wt[:, 1] - t0) / 100.0  # microseconds
 dur = en - st
@@ -38,3 +38,10 @@ for f in np.linspace(0, 1, 21)[:-1]:
     t = f * T
     print(f"t={t:8.0f}us active waves {int(((st <= t) & (en > t)).sum()):6d}")
 print("slowest wave durations (us):", [int(d) for d in np.sort(dur)[-10:]])
+# block occupancy: a 4-wave block holds its slots until its last wave ends
+blk = wt_all[: (len(wt_all) // 4) * 4].reshape(-1, 4, 2)
+blk = blk[(blk[:, :, 1] > 0).all(1)]
+span = blk[:, :, 1].max(1) - blk[:, :, 0].min(1)
+busy = (blk[:, :, 1] - blk[:, :, 0]).sum(1)
+print(f"blocks {len(blk)}: wave-slot time idle inside blocks {1 - busy.sum() / (4 * span.sum()):.3f} "
+      f"(waves ending before their block's last wave)")

@@ -120,6 +120,8 @@ SIGNATURES = {
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
     "rt_on_render_wait": (c_int, []),
     "rt_on_shutdown": (c_int, []),
+    "rt_image_write_ppm": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
+    "rt_image_write_png": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
 }
 
 _LIB: Optional[ctypes.CDLL] = None
@@ -365,3 +367,19 @@ def on_render_wait() -> None:
 
 def on_shutdown() -> None:
     _check(lib().rt_on_shutdown(), "rt_on_shutdown")
+
+
+# ------------------------------------------------------------ output path
+RT_IMAGE_FLIP_Y = 1
+
+
+def write_image(image: np.ndarray, path, flip_y: bool = True) -> None:
+    """Writes an (H, W) uint32 RGBA8 host frame (rt_on_render / rt_trace's
+    CurrentImage) as PPM or PNG by the path's suffix (rt_image_write_ppm /
+    rt_image_write_png); flip_y: on-screen orientation (row H-1 first)."""
+    assert image.dtype == np.uint32 and image.ndim == 2 and image.flags.c_contiguous
+    img = RtImage(image.ctypes.data, image.shape[1], image.shape[0], RT_FORMAT_R8G8B8A8_U32)
+    path = str(path)
+    fn = lib().rt_image_write_png if path.lower().endswith(".png") else lib().rt_image_write_ppm
+    name = "rt_image_write_png" if path.lower().endswith(".png") else "rt_image_write_ppm"
+    _check(fn(ctypes.byref(img), path.encode(), RT_IMAGE_FLIP_Y if flip_y else 0), name)

@@ -42,6 +42,7 @@ struct rt_device {
     // where the denser 256-sphere scene leaves the waves' secondary rays too
     // incoherent for a wave-wide cluster skip)
     int clusters_env = 1;
+    int interleave_env = 0;  // RT_INTERLEAVE=1: wave tiles interleaved over the block tile (P >= 2)
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
@@ -116,6 +117,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (to && to[0] == '0') d->tile_sched = 0;
     const char *clu = getenv("RT_CLUSTERS");
     if (clu && (clu[0] == '0' || clu[0] == '2')) d->clusters_env = clu[0] - '0';
+    const char *il = getenv("RT_INTERLEAVE");
+    if (il && (il[0] == '0' || il[0] == '1')) d->interleave_env = il[0] - '0';
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -679,6 +682,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // With heaviest-first scheduling each launch also measures its tiles and
     // re-sorts them for the next launch (live tiles keep costs > 0, dead ones
     // 0, so the live prefix is preserved).
+    a.interleave = d->interleave_env && lpp >= 2 ? 1u : 0u;
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     const bool cull = d->cull != 0;
@@ -687,6 +691,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.tiles_x = rtk_tiles_x(desc->Width, lpp);
     std::vector<uint32_t> key = {desc->Width, desc->Height, local_rows, band_rows, band_count, desc->BandIndex,
                                  (uint32_t)lpp, (uint32_t)rs, (uint32_t)cull, (uint32_t)empty_capable, (uint32_t)sched,
+                                 a.interleave,
                                  (uint32_t)d->scene_gen, (uint32_t)(d->scene_gen >> 32)};
     for (const float *f : {a.cam_pos, a.cam_x, a.cam_y, a.film_center}) {
         for (int i = 0; i < 3; ++i) {

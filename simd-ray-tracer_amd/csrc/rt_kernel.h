@@ -55,6 +55,7 @@ struct TraceArgs {
     const float4 *clusters;      // optional: clustered prefilter table (kClEntryF4 rows per entry)
     uint32_t n_cpairs;           // cluster-pair entries at its start; 0 = per-group prefilter loop
     uint32_t cl_words;           // u64 words of the clustered loop's pair mask (1 or 2)
+    uint32_t interleave;         // wave tiles interleave over the block tile (P >= 2 only)
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,

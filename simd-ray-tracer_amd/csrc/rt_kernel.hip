@@ -533,7 +533,8 @@ __device__ __forceinline__ void set_pair(uint64_t (&wave)[2], bool any, uint32_t
 
 template <int W>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
-                                             uint64_t (&wave)[2]) {
+                                             uint64_t (&wave)[2], PfStats *ps) {
+    if (ps) ps->groups += count;
     for (uint32_t m = first; m < first + count; ++m) {
         cv4f_t *e = ct + kClEntryF4 * m;
         const v4f_t r0 = e[0], r1 = e[1];
@@ -544,9 +545,11 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
     }
 }
 
+// ps (RTK_STATS): groups += member-pair entries tested, pairs += sphere pairs
+// rechecked exactly, lane_pairs += clusters entered (per wave).
 template <bool SIMD, int W>
 __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray,
-                                                 Hit &h) {
+                                                 Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[2] = {0ull, 0ull};
     for (uint32_t c = 0; c < a.n_cpairs; ++c) {
@@ -556,8 +559,9 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
         const bool in0 = __ballot(!(v.x >= r1.z)) != 0;
         const bool in1 = __ballot(!(v.y >= r1.w)) != 0;
-        if (in0) member_pairs<W>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave);
-        if (in1) member_pairs<W>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave);
+        if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
+        if (in0) member_pairs<W>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
+        if (in1) member_pairs<W>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);
     }
     cv4f_t *gp = (cv4f_t *)a.groups;
 #pragma unroll
@@ -568,6 +572,7 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
             const uint32_t g = 32u * (uint32_t)w + (q >> 1);
             const bool f01 = (m >> q) & 1u, f23 = (m >> (q + 1u)) & 1u;
             m &= ~(3ull << q);
+            if (ps) ps->pairs += (f01 ? 1u : 0u) + (f23 ? 1u : 0u);
             recheck_pairs<SIMD>(a, lds_groups, load_group_pf_at(gp + kGroupF4 * g), g, ray, h, f01, f23);
         }
     }
@@ -751,11 +756,13 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     const uint32_t tile = a.tile_order ? a.tile_order[blk] : blk;
     const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
     const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t x0 = tile_x * (2u * TW) + (wave & 1u) * TW;
-    const uint32_t ly0 = tile_y * (2u * TH) + (wave >> 1) * TH;
     const uint32_t pl = lane / P, j = lane % P;  // pixel of the tile, sample lane of the pixel
-    const uint32_t x = x0 + pl % TW;
-    const uint32_t ly = ly0 + pl / TW;
+    // wave tile: a TW x TH quadrant of the block tile, or (interleave) every
+    // other pixel and row of the whole block tile, parity (wave & 1, wave >> 1)
+    const uint32_t x = a.interleave ? tile_x * (2u * TW) + 2u * (pl % TW) + (wave & 1u)
+                                    : tile_x * (2u * TW) + (wave & 1u) * TW + pl % TW;
+    const uint32_t ly = a.interleave ? tile_y * (2u * TH) + 2u * (pl / TW) + (wave >> 1)
+                                     : tile_y * (2u * TH) + (wave >> 1) * TH + pl / TW;
     const bool valid = x < a.width && ly < a.local_rows;
     const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
     const bool owner = j == 0;
@@ -886,8 +893,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
                         if (SRC == kSrcSmem && pf && a.n_cpairs) {
                             if (kStats && a.stats) st_pf_rounds += 1;
-                            if (a.cl_words == 1u) clustered_groups<SIMD, 1>(a, lds_groups, ray, h);
-                            else clustered_groups<SIMD, 2>(a, lds_groups, ray, h);
+                            PfStats *ps = kStats && a.stats ? &st_pf : nullptr;
+                            if (a.cl_words == 1u) clustered_groups<SIMD, 1>(a, lds_groups, ray, h, ps);
+                            else clustered_groups<SIMD, 2>(a, lds_groups, ray, h, ps);
                         } else if (SRC == kSrcSmem && pf) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr, p.own,
@@ -1098,14 +1106,16 @@ __global__ __launch_bounds__(256) void cull_kernel(TraceArgs a, uint32_t *live, 
     __shared__ uint32_t s_any;
     const uint32_t tile = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
-    const uint32_t x0 = tile_x * (2u * TW) + (wave & 1u) * TW;
-    const uint32_t ly0 = tile_y * (2u * TH) + (wave >> 1) * TH;
+    // the wave tile's pixel extent [x0, x1] x [ly0, ly1] (see trace_kernel)
+    const uint32_t x0 = tile_x * (2u * TW) + (a.interleave ? (wave & 1u) : (wave & 1u) * TW);
+    const uint32_t ly0 = tile_y * (2u * TH) + (a.interleave ? (wave >> 1) : (wave >> 1) * TH);
+    const uint32_t x1 = x0 + (a.interleave ? 2u : 1u) * (TW - 1u), ly1 = ly0 + (a.interleave ? 2u : 1u) * (TH - 1u);
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
-    // the wave's tile; band_rows % 8 == 0 keeps its TH rows contiguous
+    // band_rows % 8 == 0 keeps the wave tile's rows in one band (2TH <= 8 when interleaved: P >= 2)
     const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
-    const Cone c = tile_cone(a, (double)x0 - 0.501, (double)(x0 + TW - 1u) + 0.501, (double)y0 - 0.501,
-                             (double)(y0 + TH - 1u) + 0.501);
+    const Cone c = tile_cone(a, (double)x0 - 0.501, (double)x1 + 0.501, (double)y0 - 0.501,
+                             (double)(y0 + (ly1 - ly0)) + 0.501);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     bool any = false;
     for (uint32_t w = 0; w < n_words; ++w) {

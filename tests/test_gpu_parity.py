@@ -208,7 +208,7 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
 # Kernel variants selected at device creation (rt_host.cpp reads the env):
 # prefilter forced on/off, brute-force primaries, 1/2 lanes per pixel.  Every
 # variant must give the same bits as the oracle.
-VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"}, {"RT_CULL": "0"},
+VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"}, {"RT_INTERLEAVE": "1"}, {"RT_CULL": "0"},
                 {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"}, {"RT_SEC_THRESHOLD": "1"}]
 
 
