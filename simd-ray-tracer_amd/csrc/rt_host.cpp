@@ -433,10 +433,16 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
                         m[2 + w] = sphere_xyz(s, kRowY);
                         m[4 + w] = sphere_xyz(s, kRowZ);
                         m[6 + w] = sphere_r2p(s);
-                        put_u(mb + 8u + w, s >> 1);
+                        if (*words == 1u) {  // the u64 pair bit itself
+                            const uint64_t bit = 1ull << (s >> 1);
+                            put_u(mb + 8u + 2u * w, (uint32_t)bit);
+                            put_u(mb + 9u + 2u * w, (uint32_t)(bit >> 32));
+                        } else {
+                            put_u(mb + 8u + w, s >> 1);
+                        }
                     } else {
-                        m[6 + w] = -INFINITY;  // padding member: never flagged
-                        put_u(mb + 8u + w, 0xFFFFFFFFu);
+                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
+                        if (*words != 1u) put_u(mb + 8u + w, 0xFFFFFFFFu);
                     }
                 }
             }

@@ -515,20 +515,18 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // it).  A wave tests the ray against about sqrt(n) cluster bounding volumes,
 // two per packed prefilter, and only the members of a cluster some lane may
 // reach run the per-sphere prefilter; a sphere pair some lane may hit sets
-// bit (slot >> 1) of the wave's pair mask (W u64 words, SGPRs only).  The
+// bit (slot >> 1) of the wave's pair mask (W u64 words, SGPRs only; W = 1
+// tables carry the bit itself, W = 2 tables the pair index).  The
 // exact recheck then walks the flagged groups in ascending order -- the
 // reference's order, so the per-class minima, tie rules and sticky inside flags
 // come out as in the full loop.  The recheck runs on every lane: a lane whose
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
 template <int W>
-__device__ __forceinline__ void set_pair(uint64_t (&wave)[2], bool any, uint32_t q) {
+__device__ __forceinline__ void set_pair(uint64_t (&wave)[2], bool any, uint32_t q) {  // W = 2: pair index q
     const uint64_t bit = any ? 1ull << (q & 63u) : 0ull;  // padding (q = ~0) never has any
-    if (W == 1) wave[0] |= bit;
-    else {
-        wave[0] |= q < 64u ? bit : 0ull;
-        wave[1] |= q < 64u ? 0ull : bit;
-    }
+    wave[0] |= q < 64u ? bit : 0ull;
+    wave[1] |= q < 64u ? 0ull : bit;
 }
 
 template <int W>
@@ -540,8 +538,14 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2];
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
-        set_pair<W>(wave, __ballot(!(v.x >= r1.z)) != 0, __float_as_uint(r2.x));
-        set_pair<W>(wave, __ballot(!(v.y >= r1.w)) != 0, __float_as_uint(r2.y));
+        if (W == 1) {  // precomputed pair bits
+            const uint64_t b0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
+            const uint64_t b1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
+            wave[0] |= (__ballot(!(v.x >= r1.z)) != 0 ? b0 : 0ull) | (__ballot(!(v.y >= r1.w)) != 0 ? b1 : 0ull);
+        } else {
+            set_pair<W>(wave, __ballot(!(v.x >= r1.z)) != 0, __float_as_uint(r2.x));
+            set_pair<W>(wave, __ballot(!(v.y >= r1.w)) != 0, __float_as_uint(r2.y));
+        }
     }
 }
 

@@ -147,16 +147,22 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
             ms = []
             for m in range(first, first + count):
                 e = tab[m]
-                pair = e[2].view(np.uint32)
+                words = e[2].view(np.uint32)
+                one_word = len(r2) // 4 <= 32  # kernel's cl_words == 1: u64 pair bits, else pair indices
+                pair = [int(words[2 * w]) | (int(words[2 * w + 1]) << 32) for w in range(2)] if one_word else \
+                    [int(words[w]) for w in range(2)]
                 for w in range(2):
                     if np.isneginf(e[1][2 + w]):
-                        assert pair[w] == 0xFFFFFFFF
+                        assert pair[w] == (0 if one_word else 0xFFFFFFFF)
                         continue
+                    if one_word:
+                        assert pair[w] and pair[w] & (pair[w] - 1) == 0, "one pair bit per member"
+                        pair[w] = pair[w].bit_length() - 1
                     x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
                     s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
                                        (r2p == t) & live)
                     assert len(s) >= 1
-                    s = [k for k in s if pair[w] == k >> 1]
+                    s = [k for k in s if pair[w] == int(k) >> 1]
                     assert len(s) >= 1, "member pair index is not its sphere's pair in group order"
                     ms.append(s[0])
             members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
