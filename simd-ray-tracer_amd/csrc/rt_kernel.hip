@@ -700,8 +700,8 @@ struct Ring {
 };
 
 #ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) of the production (SMEM) kernels;
-#define RTK_MIN_WAVES_PER_SIMD 6   // 6 waves = 80 VGPRs: measured best on C2 (w1 55.2k, w6 57.7k,
-#endif                             // w7 57.6k, w8 56.0k Mrays/s; w7/w8 spill)
+#define RTK_MIN_WAVES_PER_SIMD 7   // 7 waves = 72 VGPRs, no VGPR spills: measured best on C2 with the
+#endif                             // cluster walk (w6 116.5k, w7 120.0-121.1k, w8 118.2k Mrays/s, w8 spills)
 
 // Work shape.  A wave owns a small pixel tile and P lanes per pixel: lane
 // j of a pixel traces that pixel's samples k = j, j+P, j+2P, ... (any order
