@@ -2,5 +2,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 for g in 2 4 8; do
-  env $EXTRA timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --sim-ranks $g 2> gpurun_out/sim.err | tail -1 || { tail -5 gpurun_out/sim.err; exit 1; }
+  env $EXTRA timeout -k 10 120 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --sim-ranks $g 2> gpurun_out/sim.err | tail -1 || { tail -5 gpurun_out/sim.err; exit 1; }
 done
