@@ -69,8 +69,9 @@ def parse():
                    help="after timing, rank 0 re-renders the whole frame alone and checks the gathered frame is "
                         "bit-identical (adds 'verified' to the line)")
     p.add_argument("--sim-ranks", type=int, default=0,
-                   help="diagnostic (1 GPU): trace only band residue 0 of this many ranks, i.e. one rank's share "
-                        "of a multi-GPU frame; prints that rank's kernel time, not a bench line")
+                   help="diagnostic (1 GPU): trace only band residue --sim-index of this many ranks, i.e. one rank's "
+                        "share of a multi-GPU frame; prints that rank's kernel time, not a bench line")
+    p.add_argument("--sim-index", type=int, default=0, help="band residue (rank) traced by --sim-ranks")
     a = p.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
@@ -151,6 +152,7 @@ def main():
     bands = args.sim_ranks if (world == 1 and args.sim_ranks > 1) else world
     rows = [rt.band_local_rows(H, band_rows, bands, r) for r in range(bands)]
     maxr = max(rows)
+    band_index = args.sim_index if bands != world else rank
     # Two frame slots: frame i's band image is gathered to rank 0 (RCCL, async)
     # while frame i+1 is traced; rank 0 assembles frame i before frame i+2
     # reuses its slot.  The timed region ends only after the last frame is
@@ -186,7 +188,8 @@ def main():
             ev[i][0].record(stream)
         dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur[slot].data_ptr(),
                   rays_ptr=rays.data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
-                  band_rows=band_rows, band_count=bands, band_index=rank, accum_zero=True, stream=stream.cuda_stream)
+                  band_rows=band_rows, band_count=bands, band_index=band_index, accum_zero=True,
+                  stream=stream.cuda_stream)
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:  # RCCL gather of the band images to rank 0 over xGMI, then assembly
@@ -236,7 +239,8 @@ def main():
 
     if bands != world:
         if rank == 0:
-            print(json.dumps({"sim_ranks": bands, "rank0_rows": rows[0], "rank0_kernel_ms": round(kern_ms, 3),
+            print(json.dumps({"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
+                              "rank0_kernel_ms": round(kern_ms, 3),
                               "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}))
         dev.close()
         return

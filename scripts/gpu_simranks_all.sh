@@ -1,0 +1,7 @@
+# Every rank's share of a G-GPU C2 frame traced alone on this GPU: bash scripts/gpu_simranks_all.sh <G> [ENV=..]
+set -o pipefail
+mkdir -p gpurun_out
+g=$1; shift
+for r in $(seq 0 $((g - 1))); do
+  env "$@" RT_X=0 timeout -k 10 120 python bench.py --steps 5 --warmup 3 --no-cpu-baseline --sim-ranks $g --sim-index $r 2> gpurun_out/sim.err | tail -1 || { tail -5 gpurun_out/sim.err; exit 1; }
+done

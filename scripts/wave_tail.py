@@ -38,6 +38,8 @@ for f in np.linspace(0, 1, 21)[:-1]:
     t = f * T
     print(f"t={t:8.0f}us active waves {int(((st <= t) & (en > t)).sum()):6d}")
 print("slowest wave durations (us):", [int(d) for d in np.sort(dur)[-10:]])
+late = np.argsort(en)[-10:]
+print("last-ending waves (start, dur) us:", [(int(st[i]), int(dur[i])) for i in late])
 # block occupancy: a 4-wave block holds its slots until its last wave ends
 blk = wt_all[: (len(wt_all) // 4) * 4].reshape(-1, 4, 2)
 blk = blk[(blk[:, :, 1] > 0).all(1)]

@@ -124,7 +124,7 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
     if (lp) {
         const int v = atoi(lp);
-        d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
+        d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
     }
     const char *st = getenv("RT_STATS");
     if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatSlots * sizeof(unsigned long long)) == hipSuccess)
@@ -655,16 +655,6 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         a.cl_words = d->cl_words[rs];
     }
     a.stats = d->d_stats;
-    if (d->want_wave_times) {
-        const size_t waves = (size_t)((desc->Width + 7u) / 8u) * ((local_rows + 7u) / 8u) * 4u * 4u;  // >= any shape
-        if (waves > d->wave_times_cap) {
-            (void)hipFree(d->d_wave_times);
-            d->d_wave_times = nullptr;
-            if (hipMalloc(&d->d_wave_times, waves * 16u) != hipSuccess) return fail(RT_ENOMEM, "wave_times");
-            d->wave_times_cap = waves;
-        }
-        a.wave_times = d->d_wave_times;
-    }
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     // Lanes per pixel (measured on MI355X at 1/2/4/8-way band splits of C2,
@@ -688,6 +678,16 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // With heaviest-first scheduling each launch also measures its tiles and
     // re-sorts them for the next launch (live tiles keep costs > 0, dead ones
     // 0, so the live prefix is preserved).
+    if (d->want_wave_times) {  // one {start, end} per wave of this launch's tile shape
+        const size_t waves = (size_t)rtk_tile_count(desc->Width, local_rows, lpp) * 4u;
+        if (waves > d->wave_times_cap) {
+            (void)hipFree(d->d_wave_times);
+            d->d_wave_times = nullptr;
+            if (hipMalloc(&d->d_wave_times, waves * 16u) != hipSuccess) return fail(RT_ENOMEM, "wave_times");
+            d->wave_times_cap = waves;
+        }
+        a.wave_times = d->d_wave_times;
+    }
     a.interleave = d->interleave_env && lpp >= 2 ? 1u : 0u;
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;

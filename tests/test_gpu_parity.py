@@ -281,7 +281,7 @@ def test_cone_culling_is_exact_at_full_resolution(rt, orc, torch_cuda, monkeypat
         assert torch_cuda.equal(g[0], ref[0]) and torch_cuda.equal(g[1], ref[1]) and g[2] == ref[2], key
 
 
-@pytest.mark.parametrize("lpp", ["4", "16"])
+@pytest.mark.parametrize("lpp", ["4", "16", "32"])
 def test_tile_order_from_previous_launch_keeps_every_bit(rt, orc, torch_cuda, monkeypatch, lpp):
     """Repeated launches of one geometry run their tiles heaviest-first (order
     learned from the previous launch): the image, the accumulation and the ray
