@@ -230,7 +230,10 @@ int rt_device_synchronize(rt_device *dev);
  * mask load, barrier, and post-barrier setup, [16] prefiltered secondary
  * wave-iterations, [17]/[18] (wave, group) pairs the prefilter flagged, with
  * and without flags on the sphere a diffuse ray just left, [19]/[20] the same
- * per sphere pair, [21] lane-level flagged pairs; [22, 32) reserved.
+ * per sphere pair, [21] lane-level flagged pairs (clustered loop: [17] member
+ * pairs tested, [19] pairs rechecked, [21] clusters entered); [22]-[24] lanes of
+ * primary rounds blocked by the sample ring, waiting for a secondary round,
+ * and done; [25, 32) reserved.
  * Returns 1 when enabled, 0 when not (out zeroed), < 0 on error. */
 int rt_debug_stats(rt_device *dev, uint64_t out[32], int reset);
 

@@ -62,7 +62,8 @@ struct TraceArgs {
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
        kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatPfRounds, kStatPfGroups,
-       kStatPfGroupsNoOwn, kStatPfPairs, kStatPfPairsNoOwn, kStatPfLanePairs, kStatCount = 22 };
+       kStatPfGroupsNoOwn, kStatPfPairs, kStatPfPairsNoOwn, kStatPfLanePairs, kStatPriBlocked, kStatPriWaitSec,
+       kStatPriDone, kStatCount = 25 };
 constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 
 // Dynamic LDS per block: rsqrt table + fold table + groups + materials.

@@ -794,6 +794,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
     uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
+    uint32_t st_pri_blocked = 0, st_pri_waitsec = 0, st_pri_done = 0;
     uint64_t st_cyc_pri = 0, st_cyc_sec = 0, st_cyc_fold = 0, st_cyc_setup = 0;
     uint64_t st_cyc_cull = 0, st_cyc_sync = 0, st_cyc_post = 0;
     PfStats st_pf = {0, 0, 0, 0, 0};
@@ -861,8 +862,14 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 if (do_sec && __builtin_popcountll(sec) < 16) { st_sparse_it += 1; st_sparse_lanes += __builtin_popcountll(sec); }
-                if (do_sec && __ballot(mode == 0u) == 0) st_tail_it += 1;  // no samples left to start at all
-                else { st_pri_it += 1; st_pri_lanes += __builtin_popcountll(pri); }
+                if (do_sec && __ballot(mode == 0u) == 0) st_tail_it += 1;  // no lane has a sample to start
+                if (!do_sec) {  // a primary round: where the other lanes are
+                    st_pri_it += 1;
+                    st_pri_lanes += __builtin_popcountll(pri);
+                    st_pri_blocked += __builtin_popcountll(__ballot(mode == 0u && !can_start));
+                    st_pri_waitsec += __builtin_popcountll(sec);
+                    st_pri_done += __builtin_popcountll(__ballot(mode == 2u));
+                }
             }
             const bool traces = do_sec ? mode == 1u : can_start;
             if (a.max_bounce != 0) nrays += __builtin_popcountll(__ballot(traces));
@@ -1064,6 +1071,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatPfPairs, (unsigned long long)st_pf.pairs);
         atomicAdd(a.stats + kStatPfPairsNoOwn, (unsigned long long)st_pf.pairs_noown);
         atomicAdd(a.stats + kStatPfLanePairs, (unsigned long long)st_pf.lane_pairs);
+        atomicAdd(a.stats + kStatPriBlocked, (unsigned long long)st_pri_blocked);
+        atomicAdd(a.stats + kStatPriWaitSec, (unsigned long long)st_pri_waitsec);
+        atomicAdd(a.stats + kStatPriDone, (unsigned long long)st_pri_done);
     }
 }
 
