@@ -28,6 +28,8 @@ CASES = [
     ("ragged_n13_37x23x3", 1, 13, 37, 23, 3, 6, True, "pixel"),
     ("survey_scene1_stream_256x4", 1, None, 256, 256, 4, 5, True, "stream"),
     ("survey_n64_pixel_256x4", 1, 64, 256, 256, 4, 8, True, "pixel"),
+    # BASELINE.json configs[1] (C2) at full size: the whole 1920x1080 frame, 256 spp
+    ("c2_full_1920x1080x256", 1, 64, 1920, 1080, 256, 8, True, "pixel"),
 ]
 
 
