@@ -4,7 +4,7 @@ configurations the parity tests use.  These are REGRESSION vectors of the
 oracle (which is itself pinned to the reference by test_oracle_reference.py),
 committed so the GPU path can be checked against fixed data too.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case ...]   (only the named cases are re-rendered)
 """
 import json
 import pathlib
@@ -15,6 +15,8 @@ import numpy as np
 ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 from oracle import oracle as orc  # noqa: E402
+
+OUT = ROOT / "tests" / "golden" / "oracle_regression.json"
 
 CASES = [
     # name, scene, N, W, H, frames, bounces, simd, seed mode
@@ -30,7 +32,11 @@ CASES = [
     ("survey_n64_pixel_256x4", 1, 64, 256, 256, 4, 8, True, "pixel"),
     # BASELINE.json configs[1] (C2) at full size: the whole 1920x1080 frame, 256 spp
     ("c2_full_1920x1080x256", 1, 64, 1920, 1080, 256, 8, True, "pixel"),
+    # configs[2] (C3) at full size: ~16x C2 on the CPU (minutes), so its CPU
+    # re-render runs only with RT_SLOW_ORACLE=1 (tests/test_golden_regression.py)
+    ("c3_full_3840x2160x1024", 1, 64, 3840, 2160, 1024, 8, True, "pixel"),
 ]
+SLOW = {"c3_full_3840x2160x1024"}
 
 
 def render_case(scene, n, W, H, frames, bounces, simd, seed):
@@ -44,7 +50,12 @@ def render_case(scene, n, W, H, frames, bounces, simd, seed):
 
 def main():
     out = {}
+    keep = json.loads(OUT.read_text()) if OUT.exists() else {}
+    only = set(sys.argv[1:])  # optional: regenerate just these cases
     for name, scene, n, W, H, frames, bounces, simd, seed in CASES:
+        if only and name not in only and name in keep:
+            out[name] = keep[name]
+            continue
         prev, cur, rays = render_case(scene, n, W, H, frames, bounces, simd, seed)
         mid = (H // 2) * W + W // 2
         out[name] = {"scene": scene, "spheres": n, "width": W, "height": H, "frames": frames, "bounces": bounces,
@@ -52,9 +63,8 @@ def main():
                      "fnv1a64_rgba8": f"{orc.fnv1a64(cur):016x}", "fnv1a64_v4": f"{orc.fnv1a64(prev):016x}",
                      "center_rgba8": f"{int(cur[mid]):08x}",
                      "center_v4_bits": [f"{int(v):08x}" for v in prev[mid].view(np.uint32)]}
-    path = ROOT / "tests" / "golden" / "oracle_regression.json"
-    path.write_text(json.dumps(out, indent=1) + "\n")
-    print(f"wrote {path} ({len(out)} cases)")
+    OUT.write_text(json.dumps(out, indent=1) + "\n")
+    print(f"wrote {OUT} ({len(out)} cases)")
 
 
 if __name__ == "__main__":

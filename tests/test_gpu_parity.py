@@ -172,6 +172,25 @@ def test_full_hd_rows_match_oracle(rt, orc, torch_cuda, gdev):
         assert np.array_equal(gc[y0:y0 + 2], oc), y0
 
 
+def test_c5_rows_match_oracle(rt, orc, torch_cuda, gdev):
+    """C5's geometry at full size (7680x4320, 256 spheres, 16 bounces; 4 of its
+    4096 spp -- later frames run the same code with other seeds): rows across
+    the frame match the oracle, which renders only those rows."""
+    s, o = _scenes(rt, orc, 1, 256)
+    W, H, S, B = 7680, 4320, 4, 16
+    cam = rt.camera_setup(s, W, H)
+    gp, gc, _ = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=S, bounces=B)
+    gp = gp.cpu().numpy().reshape(H, W, 4)
+    gc = gc.cpu().numpy().view(np.uint32).reshape(H, W)
+    ocam = orc.camera(o, W, H)
+    for y0 in (0, 2161, 4318):
+        op, oc, _ = orc.render(o, ocam, W, H, frames=S, max_bounce=B, rows=(y0, y0 + 2), threads=orc.cpu_threads())
+        op = op.reshape(H, W, 4)[y0:y0 + 2]
+        oc = oc.reshape(H, W)[y0:y0 + 2]
+        assert np.array_equal(gp[y0:y0 + 2].view(np.uint32), op.view(np.uint32)), y0
+        assert np.array_equal(gc[y0:y0 + 2], oc), y0
+
+
 def test_on_render_progressive_driver(rt, orc, torch_cuda):
     """OnRender semantics (main.cpp:705-859): first call resets and renders
     frame 0 without output; each later call returns the previous COMPLETED
