@@ -259,7 +259,7 @@ int64_t rt_debug_masks(rt_device *dev, uint64_t *out, uint64_t max_words);
 int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p, uint32_t capacity,
                        uint32_t *out_count, uint32_t *out_flags);
 /* The clustered secondary-ray prefilter table rt_scene_upload builds for one
- * rule set (layout: rt_kernel.h, kClEntryF4 = 3 float4 rows per entry;
+ * rule set (layout: rt_kernel.h, kClEntryF4 = 4 float4 rows per entry;
  * cluster-pair entries first).  *out_f4 = float4 rows, *out_cpairs = cluster
  * pairs (0: the scene uses the per-group prefilter loop).  out may be NULL to
  * query the size.  Test/inspection hook: the kernel's skip proof is checked

@@ -142,7 +142,10 @@ def lib() -> ctypes.CDLL:
         except ImportError:
             pass
         L = ctypes.CDLL(str(LIB_PATH))
+        ab_build = "RT_TRACE_LIB" in os.environ  # an older A/B build may lack newer inspection hooks
         for name, (res, args) in SIGNATURES.items():
+            if ab_build and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -243,7 +246,7 @@ def scene_prefilter(scene: RtScene, simd: bool = True):
 
 
 def scene_clusters(scene: RtScene, simd: bool = True):
-    """The clustered prefilter table rt_scene_upload builds: (table (n, 3, 4)
+    """The clustered prefilter table rt_scene_upload builds: (table (n, 4, 4)
     f32 rows, n_cpairs); n_cpairs == 0 means the per-group loop is used."""
     nf4, ncp = c_uint32(), c_uint32()
     _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), None, 0, ctypes.byref(nf4), ctypes.byref(ncp)),
@@ -252,7 +255,7 @@ def scene_clusters(scene: RtScene, simd: bool = True):
     if nf4.value:
         _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), tab.ctypes.data, nf4.value, ctypes.byref(nf4),
                                        ctypes.byref(ncp)), "rt_scene_clusters")
-    return tab.reshape(-1, 3, 4), int(ncp.value)
+    return tab.reshape(-1, 4, 4), int(ncp.value)
 
 
 def rsqrt_table_builtin() -> np.ndarray:

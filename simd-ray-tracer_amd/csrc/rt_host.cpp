@@ -377,9 +377,21 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // final clusters: f32 centres (what the kernel subtracts), exact thresholds
     struct Cl {
         float qx, qy, qz, t;
+        float b;                    // behind threshold (below)
         std::vector<uint32_t> mem;  // sphere slots, ascending
     };
     std::vector<Cl> cl;
+    // Behind thresholds: a member j cannot be accepted by a ray whose computed
+    // T_j + X_j stays below eps (it = T - X or T + X < eps), and X_j <= r_j(1+2u).
+    // With T_j within 4.2u sqrt(M_j)|D| of (S_j - O).D (one rounding in C_j, three
+    // in the dot) and the prefilter's FMA T_c within 4u sqrt(M_c)|D| of (q_c - O).D,
+    // (S_j - O).D <= (q_c - O).D + |S_j - q_c||D| gives: T_c < -b_c with
+    //   b_c = max_j (|S_j - q_c| + r_j)(1 + 2^-15) + 4.3u (sqrt(M_c) + sqrt(M_j))
+    // proves every member is behind every origin-side candidate (|D| <= 1 + 2^-17
+    // under the |D|^2 bound).  Per sphere (q_c = S_j): b_j = r_j(1 + 2^-15) + 8.6u sqrt(M_j).
+    std::vector<float> beta_of_slot(4u * n_groups, 0.0f);
+    for (const Sph &o : sp)
+        beta_of_slot[o.s] = std::nextafter((float)-(o.r * (1.0 + 0x1p-15) + 8.6 * u * std::sqrt(o.m)), -INFINITY);
     for (uint32_t c = 0; c < k; ++c) {
         Cl C;
         double sx = 0.0, sy = 0.0, sz = 0.0;
@@ -402,10 +414,16 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         const double mc = bound_m(qx, qy, qz);
         rho = (rho + u * std::sqrt(mc)) * (1.0 + 1e-6);
         C.t = std::nextafter((float)(rho * rho + mc * (32.0 * u + 1.01 * K)), INFINITY);
+        double bmax = 0.0;
+        for (uint32_t i : C.mem)
+            bmax = std::max(bmax, (std::sqrt((sp[i].x - qx) * (sp[i].x - qx) + (sp[i].y - qy) * (sp[i].y - qy) +
+                                             (sp[i].z - qz) * (sp[i].z - qz)) + sp[i].r) * (1.0 + 0x1p-15) +
+                                      4.3 * u * (std::sqrt(mc) + std::sqrt(sp[i].m)));
+        C.b = std::nextafter((float)-bmax, -INFINITY);
         for (uint32_t &i : C.mem) i = sp[i].s;
         cl.push_back(std::move(C));
     }
-    if (cl.size() & 1u) cl.push_back(Cl{0.0f, 0.0f, 0.0f, -INFINITY, {}});
+    if (cl.size() & 1u) cl.push_back(Cl{0.0f, 0.0f, 0.0f, -INFINITY, 0.0f, {}});
     const uint32_t n_cp = (uint32_t)cl.size() / 2u;
     uint32_t n_mp = 0;
     for (const Cl &C : cl) n_mp += ((uint32_t)C.mem.size() + 1u) / 2u;
@@ -421,6 +439,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         float *e = &tab[(size_t)p * kClEntryF4 * 4u];
         const Cl &A = cl[2u * p], &B = cl[2u * p + 1u];
         e[0] = A.qx, e[1] = B.qx, e[2] = A.qy, e[3] = B.qy, e[4] = A.qz, e[5] = B.qz, e[6] = A.t, e[7] = B.t;
+        e[12] = A.b, e[13] = B.b;
         const Cl *two[2] = {&A, &B};
         for (int h = 0; h < 2; ++h) {
             const uint32_t cnt = ((uint32_t)two[h]->mem.size() + 1u) / 2u;
@@ -437,6 +456,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
                         m[2 + w] = sphere_xyz(s, kRowY);
                         m[4 + w] = sphere_xyz(s, kRowZ);
                         m[6 + w] = sphere_r2p(s);
+                        m[12 + w] = beta_of_slot[s];
                         if (*words == 1u) {  // the u64 pair bit itself
                             const uint64_t bit = 1ull << (s >> 1);
                             put_u(mb + 8u + 2u * w, (uint32_t)bit);

@@ -13,15 +13,17 @@ constexpr uint32_t kRowR2 = 4;        //   r*r
 enum { kFlagAccumZero = 1 };
 // Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
 // kClEntryF4 float4 rows, read through the scalar cache --
-//   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1}
-//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bits}
+//   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1} {b0 b1 0 0}
+//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bits}                      {b0 b1 0 0}
+// (b = behind threshold: a lane whose prefilter T = (centre - O).D is below
+// it cannot accept any member -- rt_host.cpp cluster_table)
 // (first/count index member-pair entries; a member's pair q = sphere slot >> 1
 // is its sphere pair in group order, the bit it sets in the wave's pair mask).
 // The wave mask is kept in SGPRs, cl_words u64 words of it:
 //   1 (n_groups <= 32): bits = {lo, hi of 1 << q for member 0, the same for member 1}
 //   2 (n_groups <= 64): bits = {q0, q1, 0, 0}
 // padding members: threshold -inf, bits 0 / q = 0xFFFFFFFF.
-constexpr uint32_t kClEntryF4 = 3;
+constexpr uint32_t kClEntryF4 = 4;
 constexpr uint32_t kClMaxGroups = 64;   // table built up to this many groups
 constexpr uint32_t kClAutoGroups = 32;  // used by default up to this many (rt_host.cpp clusters_env)
 

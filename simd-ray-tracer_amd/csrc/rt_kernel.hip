@@ -395,8 +395,8 @@ __device__ __forceinline__ f2 pair_dist(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 
 // sphere is missed under both rule sets -- and only groups where some lane
 // fails that proof run the exact test.  A wave with any lane outside the
 // |D|^2 bound runs the exact loop instead.
-__device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz) {
-    f2 cx, cy, cz, cc, T, e;
+__device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 &T) {
+    f2 cx, cy, cz, cc, e;
     asm("v_pk_add_f32 %[cx], %[sx], %[rx] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
         "v_pk_add_f32 %[cy], %[sy], %[ry] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
         "v_pk_add_f32 %[cz], %[sz], %[rz] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
@@ -448,8 +448,9 @@ __device__ __forceinline__ void recheck_pairs(const TraceArgs &a, const float4 *
 
 // Prefilter flags of group G's two sphere pairs for this lane's ray.
 __device__ __forceinline__ void prefilter_group(const Group &G, const RayPk &p, bool &f01, bool &f23) {
-    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
-    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
+    f2 T01, T23;
+    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
+    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
     f01 = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]);
     f23 = !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
 }
@@ -469,8 +470,9 @@ __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *
     if (ps) {
         const bool mine = (own >> 2) == g;
         const uint32_t ol = own & 3u;
-        const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]});
-        const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]});
+        f2 T01, T23;
+        const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
+        const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
         const bool n01 = (!(e01.x >= G.r2p[0]) && !(mine && ol == 0u)) | (!(e01.y >= G.r2p[1]) && !(mine && ol == 1u));
         const bool n23 = (!(e23.x >= G.r2p[2]) && !(mine && ol == 2u)) | (!(e23.y >= G.r2p[3]) && !(mine && ol == 3u));
         ps->groups += __ballot(f01 | f23) != 0;
@@ -536,15 +538,18 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
     for (uint32_t m = first; m < first + count; ++m) {
         cv4f_t *e = ct + kClEntryF4 * m;
         const v4f_t r0 = e[0], r1 = e[1];
-        const v4f_t r2 = e[2];
-        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
+        const v4f_t r2 = e[2], r3 = e[3];
+        f2 T;
+        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T);
+        // a lane may hit the sphere: near the line, and not wholly behind the origin
+        const bool f0 = !(v.x >= r1.z) && !(T.x < r3.x), f1 = !(v.y >= r1.w) && !(T.y < r3.y);
         if (W == 1) {  // precomputed pair bits
             const uint64_t b0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
             const uint64_t b1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
-            wave[0] |= (__ballot(!(v.x >= r1.z)) != 0 ? b0 : 0ull) | (__ballot(!(v.y >= r1.w)) != 0 ? b1 : 0ull);
+            wave[0] |= (__ballot(f0) != 0 ? b0 : 0ull) | (__ballot(f1) != 0 ? b1 : 0ull);
         } else {
-            set_pair<W>(wave, __ballot(!(v.x >= r1.z)) != 0, __float_as_uint(r2.x));
-            set_pair<W>(wave, __ballot(!(v.y >= r1.w)) != 0, __float_as_uint(r2.y));
+            set_pair<W>(wave, __ballot(f0) != 0, __float_as_uint(r2.x));
+            set_pair<W>(wave, __ballot(f1) != 0, __float_as_uint(r2.y));
         }
     }
 }
@@ -559,10 +564,11 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
     for (uint32_t c = 0; c < a.n_cpairs; ++c) {
         cv4f_t *e = ct + kClEntryF4 * c;
         const v4f_t r0 = e[0], r1 = e[1];
-        const v4f_t r2 = e[2];
-        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y});
-        const bool in0 = __ballot(!(v.x >= r1.z)) != 0;
-        const bool in1 = __ballot(!(v.y >= r1.w)) != 0;
+        const v4f_t r2 = e[2], r3 = e[3];
+        f2 T;
+        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T);
+        const bool in0 = __ballot(!(v.x >= r1.z) && !(T.x < r3.x)) != 0;
+        const bool in1 = __ballot(!(v.y >= r1.w) && !(T.y < r3.y)) != 0;
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
         if (in0) member_pairs<W>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
         if (in1) member_pairs<W>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);

@@ -27,11 +27,27 @@ def exact_dist(cx, cy, cz, dx, dy, dz):
     return (qx * qx + qy * qy) + qz * qz
 
 
-def prefilter(cx, cy, cz, dx, dy, dz):
-    """rt_kernel.hip pair_prefilter, lane by lane."""
+def prefilter(cx, cy, cz, dx, dy, dz, with_t=False):
+    """rt_kernel.hip pair_prefilter, lane by lane: e (and its FMA T)."""
     cc = fma(cx, cx, fma(cy, cy, cz * cz))
     T = fma(cz, dz, fma(cy, dy, cx * dx))
-    return fma(-T, T, cc)
+    e = fma(-T, T, cc)
+    return (e, T) if with_t else e
+
+
+def could_accept(cx, cy, cz, dx, dy, dz, r2, simd):
+    """main.cpp:401-429 per sphere with every f32 op rounded separately: the
+    exact test passes AND the candidate's it clears eps (the current minimum
+    is ignored, so this over-approximates what a lane can accept)."""
+    T = (cx * dx + cy * dy) + cz * dz
+    dist = exact_dist(cx, cy, cz, dx, dy, dz)
+    hit = (dist < r2) if simd else ~(dist > r2)
+    with np.errstate(invalid="ignore"):
+        X = np.sqrt((r2 - dist).astype(F))
+    it = T - X
+    it = np.where(it < F(1e-4), T + X, it)
+    ok = (it > F(1e-4)) if simd else ~(it < F(1e-4))
+    return hit & ok
 
 
 def unit(v):
@@ -92,6 +108,7 @@ def test_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     skipped = ~(e < r2p)
     assert not np.any(hit & skipped), "prefilter skipped a sphere the exact test accepts"
     assert hit.sum() > 0
+
     if flags & 1:  # where it is enabled, the prefilter must actually cull
         assert (~skipped).sum() < 1.5 * hit.sum() + 0.05 * hit.size
 
@@ -139,6 +156,7 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     live = np.isfinite(r2p)
     # decode the table: clusters -> member spheres (by centre and r2p) and pair indices
     members = []
+    beta_of = {}  # per-sphere behind threshold (member rows)
     for c in range(ncp):
         q = tab[c]
         u = q[2].view(np.uint32)
@@ -165,8 +183,9 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
                     s = [k for k in s if pair[w] == int(k) >> 1]
                     assert len(s) >= 1, "member pair index is not its sphere's pair in group order"
                     ms.append(s[0])
+                    beta_of[s[0]] = np.float32(e[3][w])
             members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
-                            np.float32(q[1][2 + h]), ms))
+                            np.float32(q[1][2 + h]), ms, np.float32(q[3][h])))
     covered = sorted(s for m in members for s in m[4])
     assert covered == sorted(np.flatnonzero(live)), "every hittable sphere is in exactly one cluster"
     rng = np.random.default_rng(11 + idx)
@@ -175,16 +194,23 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     cx = centres[None, :, 0] - o[:, None, 0]
     cy = centres[None, :, 1] - o[:, None, 1]
     cz = centres[None, :, 2] - o[:, None, 2]
-    dist = exact_dist(cx, cy, cz, dx, dy, dz)
-    hit = ((dist < r2) if simd else ~(dist > r2)) & live[None, :]
-    assert hit.sum() > 0
-    skipped_any = 0
-    for qx, qy, qz, t, ms in members:
+    accept = could_accept(cx, cy, cz, dx, dy, dz, r2[None, :], simd) & live[None, :]
+    assert accept.sum() > 0
+    # sphere level: near-line estimate or wholly behind the origin (member rows)
+    e_s, t_s = prefilter(cx, cy, cz, dx, dy, dz, with_t=True)
+    beta = np.array([beta_of.get(k, -np.inf) for k in range(len(r2))], F)
+    skip_s = ~(e_s < r2p[None, :]) | (t_s < beta[None, :])
+    assert not np.any(accept & skip_s), "the member test skipped a sphere a lane can accept"
+    assert np.any((t_s < beta[None, :]) & (e_s < r2p[None, :]) & live[None, :]), "the behind rule culls nothing"
+    skipped_any = behind_any = 0
+    for qx, qy, qz, t, ms, bc in members:
         if np.isneginf(t):
             continue
-        ex = prefilter((qx - o[:, 0])[:, None], (qy - o[:, 1])[:, None], (qz - o[:, 2])[:, None],
-                       d[:, 0:1], d[:, 1:2], d[:, 2:3])[:, 0]
-        skip = ~(ex < t)
+        ex, tx = prefilter((qx - o[:, 0])[:, None], (qy - o[:, 1])[:, None], (qz - o[:, 2])[:, None],
+                           d[:, 0:1], d[:, 1:2], d[:, 2:3], with_t=True)
+        behind = tx[:, 0] < bc
+        skip = ~(ex[:, 0] < t) | behind
         skipped_any += int(skip.sum())
-        assert not np.any(hit[skip][:, ms]), "a skipped cluster holds an exact hit"
-    assert skipped_any > 0  # the level does cull
+        behind_any += int((behind & (ex[:, 0] < t)).sum())
+        assert not np.any(accept[skip][:, ms]), "a skipped cluster holds a sphere a lane can accept"
+    assert skipped_any > 0 and behind_any > 0  # both cluster rules cull
