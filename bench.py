@@ -105,6 +105,19 @@ def cpu_baseline(args, n_rays_gpu_step: int):
                       f"RenderTile restatement, pixel seeds)"}
 
 
+def lanes_per_pixel(band_pixels: int, frames: int) -> int:
+    """The P rt_trace picks for a band (rt_host.cpp rt_trace; RT_LANES_PER_PIXEL overrides), for the line's label."""
+    import torch
+    forced = os.environ.get("RT_LANES_PER_PIXEL")
+    if forced in ("1", "2", "4", "8", "16", "32"):
+        return int(forced)
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    p = 4 if band_pixels >= cus * 6144 else 8 if band_pixels >= cus * 1536 else 16
+    while p > 1 and p // 2 >= frames:
+        p //= 2
+    return p
+
+
 def pmc_record(workload: str):
     """The newest committed rocprofv3 --pmc record of this workload
     (profiles/rNN_*_pmc.json, written by scripts/pmc_to_json.py)."""
@@ -257,7 +270,8 @@ def main():
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": round(pmc["hbm_bytes_per_dispatch"]) if pmc and "hbm_bytes_per_dispatch" in pmc else None,
-                "kernel": "trace_kernel<SIMD,SMEM,CULL,4>", "kernel_ms": round(kern_ms, 3),
+                "kernel": f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{lanes_per_pixel(rows[0] * W, S)}>",
+                "kernel_ms": round(kern_ms, 3),
                 "work_per_launch": f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d, brute force)",
                 "note": "algorithmic ops count every sphere for every segment; the kernel culls sphere groups "
                         "for primary rays exactly, so it executes fewer ops and frac may exceed 1. The "
