@@ -1,3 +1,4 @@
+# needs scripts/mb_valu: hipcc --offload-arch=gfx950 -O3 scripts/mb_valu.hip -o scripts/mb_valu (built here, travels to the box)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
