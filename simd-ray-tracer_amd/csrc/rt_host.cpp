@@ -37,10 +37,10 @@ struct rt_device {
     uint32_t n_cpairs[2] = {0, 0};               // 0: per-group prefilter loop
     uint32_t cl_words[2] = {0, 0};
     // RT_CLUSTERS=0: per-group prefilter loop only; 2: clustered loop up to
-    // kClMaxGroups groups; default 1: up to kClAutoGroups (measured on C2
-    // geometry: clusters win 13-15 % at 16/24/32 groups and lose 18 % at 64,
-    // where the denser 256-sphere scene leaves the waves' secondary rays too
-    // incoherent for a wave-wide cluster skip)
+    // kClMaxGroups groups; default 1: up to kClAutoGroups (measured: clusters
+    // win 13-15 % at 16/24/32 groups on C2 geometry, and at C5's 64 groups
+    // 32.4k against 28.6k Mrays/s once the behind rule and the 7-block LDS
+    // image are in)
     int clusters_env = 1;
     int interleave_env = 0;  // RT_INTERLEAVE=1: wave tiles interleaved over the block tile (P >= 2)
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
@@ -301,9 +301,10 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     const double u = 0x1p-24, K = 0x1p-16;
     for (Sph &o : sp) o.m = bound_m(o.x, o.y, o.z);
     auto sigma = [&](const Sph &o) { return std::sqrt(o.r * o.r + 13.3 * u * o.m) + u * std::sqrt(o.m); };
-    // ~1.25 sqrt(n) clusters: measured on C2 (N = 64) K = 6/8/10/12/16 ->
-    // 112.4k/113.8k/114.6k/114.5k/111.4k Mrays/s
-    uint32_t k = std::max(2u, (uint32_t)std::lround(1.25 * std::sqrt((double)n)));
+    // max(1.25 sqrt(n), n/8) clusters: measured on C2 (N = 64) K = 6/8/10/12/16 ->
+    // 112.4k/113.8k/114.6k/114.5k/111.4k Mrays/s; at 200 spheres K = 17/28 ->
+    // 45.0k/46.9k; at C5 (256) K = 20/26/32/40 -> 30.1k/31.3k/32.4k/32.4k
+    uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / 8u));
     if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob
     // k-means (f64, fixed LCG restarts) minimising the sum of rho_c^2
     std::vector<uint32_t> best_lab;
@@ -713,6 +714,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         a.wave_times = d->d_wave_times;
     }
     a.interleave = d->interleave_env && lpp >= 2 ? 1u : 0u;
+    a.lut_in_lds = rtk_lut_in_lds(a.n_groups) ? 1u : 0u;
+    a.fold_in_lds = rtk_fold_in_lds(a.n_groups) ? 1u : 0u;
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     const bool cull = d->cull != 0;

@@ -25,7 +25,7 @@ enum { kFlagAccumZero = 1 };
 // padding members: threshold -inf, bits 0 / q = 0xFFFFFFFF.
 constexpr uint32_t kClEntryF4 = 4;
 constexpr uint32_t kClMaxGroups = 64;   // table built up to this many groups
-constexpr uint32_t kClAutoGroups = 32;  // used by default up to this many (rt_host.cpp clusters_env)
+constexpr uint32_t kClAutoGroups = 64;  // used by default up to this many (rt_host.cpp clusters_env)
 
 // HBM layout of an uploaded scene (per rule set):
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
@@ -60,6 +60,8 @@ struct TraceArgs {
     uint32_t n_cpairs;           // cluster-pair entries at its start; 0 = per-group prefilter loop
     uint32_t cl_words;           // u64 words of the clustered loop's pair mask (1 or 2)
     uint32_t interleave;         // wave tiles interleave over the block tile (P >= 2 only)
+    uint32_t lut_in_lds;         // rsqrt table in the LDS image (else read from HBM: rtk_lut_in_lds)
+    uint32_t fold_in_lds;        // running-mean weight table in the LDS image (else computed: rtk_fold_in_lds)
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
@@ -68,9 +70,17 @@ enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriG
        kStatPriDone, kStatCount = 25 };
 constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 
-// Dynamic LDS per block: rsqrt table + fold table + groups + materials.
+// Dynamic LDS per block: [rsqrt table] + fold table + groups + materials.
+// The 8 KB table stays in LDS up to 32 groups; a larger scene's image would
+// cost occupancy (C5's 64 groups: 5 -> 7 blocks per CU without it and the
+// weight table), so the table is then read from HBM through the caches.
+// The 2 KB weight table of the first 256 frames goes the same way (the
+// weights are then two divisions per sample): C5 fits 7 blocks per CU.
+static inline bool rtk_lut_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
+static inline bool rtk_fold_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
 static inline size_t rtk_lds_bytes(uint32_t n_groups) {
-    return 8192u + 2048u + (size_t)n_groups * (16u * kGroupF4) + (size_t)n_groups * 128u;
+    return (rtk_lut_in_lds(n_groups) ? 8192u : 0u) + (rtk_fold_in_lds(n_groups) ? 2048u : 0u) +
+           (size_t)n_groups * (16u * kGroupF4) + (size_t)n_groups * 128u;
 }
 static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4 + 128u);  // 265 groups
 

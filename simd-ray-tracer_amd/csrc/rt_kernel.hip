@@ -121,11 +121,19 @@ __device__ __forceinline__ void normalize(float &x, float &y, float &z) {
 
 // rsqrtss (x64_math.h:71-74) from the 2x1024 table: exponent parity + top
 // 10 mantissa bits pick the entry, the remaining even exponent scales it.
-__device__ __forceinline__ float rsqrt_x86(const float *lut, float v) {
+// The table sits in the block's LDS image, or (large scenes, in_lds false:
+// the LDS budget goes to occupancy) is read from HBM through the caches.
+struct Lut {
+    const float *lds, *glob;
+    bool in_lds;  // wave-uniform
+};
+
+__device__ __forceinline__ float rsqrt_x86(const Lut &lut, float v) {
     const uint32_t u = __float_as_uint(v);
     const int32_t e = (int32_t)((u >> 23) & 0xFFu) - 127;
     const uint32_t par = (uint32_t)e & 1u;
-    const float base = lut[par * 1024u + ((u >> 13) & 1023u)];
+    const uint32_t idx = par * 1024u + ((u >> 13) & 1023u);
+    const float base = lut.in_lds ? lut.lds[idx] : lut.glob[idx];
     const int32_t sh = (e - (int32_t)par) >> 1;
     return __uint_as_float(__float_as_uint(base) - ((uint32_t)sh << 23));
 }
@@ -194,7 +202,7 @@ __device__ __forceinline__ void start_sample(const TraceArgs &a, uint32_t x, uin
 }
 
 // Emission, attenuation and the next direction (main.cpp:446-481).
-__device__ __forceinline__ void shade(const float *lut, float4 col_spec, float4 emis_ior, float hx, float hy, float hz,
+__device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 emis_ior, float hx, float hy, float hz,
                                       bool inside, Sample &p) {
     p.cx = p.cx + emis_ior.x * p.ax;
     p.cy = p.cy + emis_ior.y * p.ay;
@@ -738,17 +746,20 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
     __shared__ float4 s_ring[P > 1 ? kWavesPerBlock * kRing * kRingStride : 1];
-    const float *lut = reinterpret_cast<const float *>(smem);
-    float2 *fold = reinterpret_cast<float2 *>(smem + 512);
-    float4 *lds_groups = smem + 512 + kFoldTable / 2;
+    const uint32_t lut_f4 = a.lut_in_lds ? 512u : 0u;  // see rtk_lds_bytes
+    const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, a.lut_in_lds != 0u};
+    float2 *fold = reinterpret_cast<float2 *>(smem + lut_f4);
+    // running-mean weights of the first kFoldTable frames (large scenes: none, computed per sample)
+    const uint32_t fold_n = a.fold_in_lds ? kFoldTable : 0u;
+    float4 *lds_groups = smem + lut_f4 + fold_n / 2;
     float4 *lds_mats = lds_groups + kGroupF4 * a.n_groups;
     {
         const float4 *glut = reinterpret_cast<const float4 *>(a.rsqrt_lut);
-        for (uint32_t i = threadIdx.x; i < 512u; i += blockDim.x) smem[i] = glut[i];
+        for (uint32_t i = threadIdx.x; i < lut_f4; i += blockDim.x) smem[i] = glut[i];
         for (uint32_t i = threadIdx.x; i < kGroupF4 * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
         for (uint32_t i = threadIdx.x; i < 8u * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
         // running-mean weights of frame k (main.cpp:484-487): 1/(p+1), p/(p+1)
-        for (uint32_t i = threadIdx.x; i < kFoldTable; i += blockDim.x) {
+        for (uint32_t i = threadIdx.x; i < fold_n; i += blockDim.x) {
             const uint32_t pc = a.prev_count + i;
             fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
         }
@@ -823,7 +834,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         if (valid && owner && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
             for (uint32_t q = 0; q < a.frames; ++q) {
                 float ratio;
-                if (q < kFoldTable) {
+                if (q < fold_n) {
                     ratio = fold[q].y;
                 } else {
                     const uint32_t pc = a.prev_count + q;
@@ -982,8 +993,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     if (P == 1) {
                         // ---- running-mean blend (main.cpp:484-489), in order by construction
                         const uint32_t pc = a.prev_count + k;
-                        const float inv = k < kFoldTable ? fold[k].x : 1.0f / (float)(pc + 1u);
-                        const float ratio = k < kFoldTable ? fold[k].y : (float)pc / (float)(pc + 1u);
+                        const float inv = k < fold_n ? fold[k].x : 1.0f / (float)(pc + 1u);
+                        const float ratio = k < fold_n ? fold[k].y : (float)pc / (float)(pc + 1u);
                         accx = ox * inv + accx * ratio;
                         accy = oy * inv + accy * ratio;
                         accz = oz * inv + accz * ratio;
@@ -992,8 +1003,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         // park Out*(1/n) and the ratio (n-1)/n of sample k's blend; the
                         // sign bit of .w marks the slot ready (the ratio is >= 0)
                         const uint32_t pc = a.prev_count + k;
-                        float2 w = fold[k < kFoldTable ? k : 0u];
-                        if (__builtin_expect(k >= kFoldTable, 0))
+                        float2 w = fold[k < fold_n ? k : 0u];  // (fold_n = 0: an unused in-bounds read)
+                        if (__builtin_expect(k >= fold_n, 0))
                             w = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
                         ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
