@@ -175,7 +175,19 @@ struct Sample {
 };
 
 // Jittered primary ray (main.cpp:375-385).
-__device__ __forceinline__ void start_sample(const TraceArgs &a, uint32_t x, uint32_t y, uint32_t frame, Sample &p) {
+// The kernel's by-value TraceArgs re-read from the kernarg segment (scalar
+// loads, K$ hits) at each use: the camera fields start_sample needs are then
+// not held in SGPRs across the trace loop, where they were spilled to VGPR
+// lanes and restored with ~30 v_readlane per primary round.
+typedef const __attribute__((address_space(4))) TraceArgs cargs_t;
+__device__ __forceinline__ cargs_t &kernel_args() {
+    cargs_t *p = (cargs_t *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));  // opaque per use: the loads stay at the use site
+    return *p;
+}
+
+template <typename Args>
+__device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t y, uint32_t frame, Sample &p) {
     p.rng = seed_mix(((uint64_t)frame * a.height + y) * a.width + x);
     const float jx = rand_float(p.rng, -0.5f, kInvRange1);
     const float jy = rand_float(p.rng, -0.5f, kInvRange1);
@@ -891,7 +903,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             const bool traces = do_sec ? mode == 1u : can_start;
             if (a.max_bounce != 0) nrays += __builtin_popcountll(__ballot(traces));
             if (traces) {
-                if (!do_sec) start_sample(a, x, y, a.prev_count + k, p);
+                if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
                 bool done;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
