@@ -173,6 +173,8 @@ int rt_scene_upload(rt_device *dev, const rt_scene *scene);
 
 #define RT_SEED_PIXEL 1u        /* per-(pixel, frame) PCG seed (GPU parity mode) */
 #define RT_FLAG_ACCUM_ZERO 1u   /* PreviousImage treated as all-zero (not read) */
+#define RT_FLAG_SRGB_POW 2u     /* RGBA8 through LinearToSRGB's exact-pow branch (main.cpp:320-321, '#if 0'
+                                   in the reference) instead of its sqrt one; PreviousImage is unaffected */
 
 typedef struct rt_trace_desc {
     uint32_t Width, Height;   /* full image (CurrentImage.Width/Height)          */
@@ -206,6 +208,13 @@ uint32_t rt_band_local_rows(uint32_t height, uint32_t band_rows, uint32_t band_c
  * synchronises the old stream when it changes. */
 int rt_trace(rt_device *dev, const rt_camera_info *cam, const rt_trace_desc *desc,
              uint64_t *d_rays, void *stream);
+
+/* ColorFromV4(LinearToSRGB(v)) (main.cpp:312-346, the store at :490) over a
+ * device-resident running mean: n_pixels v4 f32 -> RGBA8, both DEVICE
+ * pointers, enqueued on `stream` (NULL: the null stream).  flags: 0 or
+ * RT_FLAG_SRGB_POW.  rt_trace already stores the RGBA8 of every frame it
+ * folds; this re-encodes a gathered or saved accumulation without tracing. */
+int rt_encode_rgba8(const float *d_accum_v4, uint32_t *d_rgba8, uint64_t n_pixels, uint32_t flags, void *stream);
 
 /* Multi-GPU gather helper: scatters `band_count` compact band images
  * (device, `elem_bytes` per pixel; rank r's image starts at byte

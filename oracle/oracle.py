@@ -57,6 +57,9 @@ def lib() -> ctypes.CDLL:
         L.or_horizontal_min.restype = c_float
         L.or_horizontal_min.argtypes = [c_void_p, c_void_p]
         L.or_cross.argtypes = [c_void_p] * 3
+        L.or_encode_rgba8.argtypes = [c_void_p, c_void_p, c_uint64, c_int]
+        L.or_srgb_channel.restype = c_float
+        L.or_srgb_channel.argtypes = [c_float, c_int]
         _L = L
         set_lut(np.fromfile(LUT_PATH, dtype=np.float32))
     return _L
@@ -135,6 +138,15 @@ def render(scene: Scene, cam: np.ndarray, width: int, height: int, *, prev_count
                      rows[0], rows[1], _p(prev), _p(cur), _p(rays))
     assert rc == 0, rc
     return prev, cur, int(rays[0])
+
+
+def encode_rgba8(prev_v4: np.ndarray, srgb_pow: bool = False) -> np.ndarray:
+    """main.cpp:312-346: RGBA8 (u32) of running means (..., 4) f32; srgb_pow picks
+    LinearToSRGB's exact-pow branch (main.cpp:320-321)."""
+    v = np.ascontiguousarray(prev_v4, np.float32).reshape(-1, 4)
+    out = np.empty(len(v), np.uint32)
+    lib().or_encode_rgba8(_p(v), _p(out), len(v), 1 if srgb_pow else 0)
+    return out
 
 
 def fnv1a64(a: np.ndarray) -> int:

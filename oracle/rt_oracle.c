@@ -622,6 +622,26 @@ static float srgb(float l)
     return l < 0.0031308f ? l * 12.92f : sqrtf(l);
 }
 
+/* main.cpp:320-321: the exact-pow branch ('#if 0' in the reference), as the
+ * WASM build would compile it: libm powf (musl there, glibc here -- the same
+ * algorithm), unfused (wasm32 has no FMA). */
+static float srgb_pow(float l)
+{
+    l = saturate(l);
+    return l < 0.0031308f ? l * 12.92f : 1.055f * powf(l, 1.0f / 2.4f) - 0.055f;
+}
+
+void or_encode_rgba8(const float *v4, uint32_t *rgba, uint64_t n, int pow_mode)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        const float *f = v4 + 4 * i;
+        rgba[i] = pow_mode ? to_u8(srgb_pow(f[0])) | (to_u8(srgb_pow(f[1])) << 8) | (to_u8(srgb_pow(f[2])) << 16) | (255u << 24)
+                           : to_u8(srgb(f[0])) | (to_u8(srgb(f[1])) << 8) | (to_u8(srgb(f[2])) << 16) | (255u << 24);
+    }
+}
+
+float or_srgb_channel(float l, int pow_mode) { return pow_mode ? srgb_pow(l) : srgb(l); }
+
 /* main.cpp:484-492: running-mean blend and the RGBA8 store. */
 static void blend_store(uint32_t prev_count, const float out[3], float *prev4, uint32_t *px)
 {

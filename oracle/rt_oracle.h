@@ -94,6 +94,11 @@ int or_render(const or_group *groups, uint32_t n_groups,
 
 uint64_t or_fnv1a64(const void *data, uint64_t nbytes);
 
+/* main.cpp:312-346 on its own: RGBA8 of n v4 running means; pow_mode selects
+ * LinearToSRGB's exact-pow branch (main.cpp:320-321) over its sqrt one. */
+void  or_encode_rgba8(const float *v4, uint32_t *rgba, uint64_t n, int pow_mode);
+float or_srgb_channel(float l, int pow_mode);
+
 /* Exposed pieces of the restatement, for differential tests against the
  * reference's own math layer (oracle/_ref). */
 void  or_group_test(const float o[3], const float d[3], const or_group *g, float dist_out[4], float t_out[4]);

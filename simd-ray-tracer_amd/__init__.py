@@ -29,6 +29,7 @@ LIB_PATH = _HERE / os.environ.get("RT_TRACE_LIB", "librt_trace.so")
 
 RT_SEED_PIXEL = 1
 RT_FLAG_ACCUM_ZERO = 1
+RT_FLAG_SRGB_POW = 2
 RT_FORMAT_R32B32G32A32_F32 = 1
 RT_FORMAT_R8G8B8A8_U32 = 2
 KEY_FORWARD, KEY_BACK, KEY_RIGHT, KEY_LEFT, KEY_UP, KEY_DOWN, KEY_RESET = (1, 2, 4, 8, 16, 32, 64)
@@ -107,6 +108,7 @@ SIGNATURES = {
     "rt_trace": (c_int, [c_void_p, POINTER(RtCameraInfo), POINTER(RtTraceDesc), c_void_p, c_void_p]),
     "rt_assemble_bands": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
                                   c_void_p]),
+    "rt_encode_rgba8": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "rt_device_synchronize": (c_int, [c_void_p]),
     "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "rt_debug_wave_times": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
@@ -283,7 +285,7 @@ class Device:
     def trace(self, cam: RtCameraInfo, *, width: int, height: int, prev_ptr: int, cur_ptr: int, rays_ptr: int,
               prev_count: int = 0, frames: int = 1, max_bounce: int = 5, simd: bool = True,
               band_rows: int = 32, band_count: int = 1, band_index: int = 0, accum_zero: bool = False,
-              stream: Optional[int] = None) -> None:
+              srgb_pow: bool = False, stream: Optional[int] = None) -> None:
         """Traces `frames` progressive frames into device images (raw device pointers)
         on the HIP stream handle `stream` (None/0 = the null stream)."""
         c = RtCameraInfo()
@@ -291,7 +293,8 @@ class Device:
         c.CurrentImage = RtImage(cur_ptr, width, height, RT_FORMAT_R8G8B8A8_U32)
         c.PreviousImage = RtImage(prev_ptr, width, height, RT_FORMAT_R32B32G32A32_F32)
         d = RtTraceDesc(width, height, prev_count, frames, max_bounce, 1 if simd else 0, RT_SEED_PIXEL,
-                        band_rows, band_count, band_index, RT_FLAG_ACCUM_ZERO if accum_zero else 0)
+                        band_rows, band_count, band_index,
+                        (RT_FLAG_ACCUM_ZERO if accum_zero else 0) | (RT_FLAG_SRGB_POW if srgb_pow else 0))
         _check(lib().rt_trace(self.handle, ctypes.byref(c), ctypes.byref(d), c_void_p(rays_ptr),
                               c_void_p(stream or 0)), "rt_trace")
 
@@ -343,6 +346,13 @@ def assemble_bands(compact_ptr: int, rank_stride_bytes: int, dst_ptr: int, width
     _check(lib().rt_assemble_bands(c_void_p(compact_ptr), rank_stride_bytes, c_void_p(dst_ptr), width, height,
                                    elem_bytes, band_rows, band_count, c_void_p(stream or 0)),
            "rt_assemble_bands")
+
+
+def encode_rgba8(accum_ptr: int, rgba8_ptr: int, n_pixels: int, srgb_pow: bool = False,
+                 stream: Optional[int] = None) -> None:
+    """ColorFromV4(LinearToSRGB(v)) over a device-resident running mean (main.cpp:312-346)."""
+    _check(lib().rt_encode_rgba8(c_void_p(accum_ptr), c_void_p(rgba8_ptr), n_pixels,
+                                 RT_FLAG_SRGB_POW if srgb_pow else 0, c_void_p(stream or 0)), "rt_encode_rgba8")
 
 
 # ------------------------------------------------- OnInit / OnRender mirror

@@ -666,7 +666,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.n_groups = d->n_groups[rs];
     a.n_spheres = d->n_spheres;
     a.use_sky = d->use_sky ? 1u : 0u;
-    a.flags = (desc->Flags & RT_FLAG_ACCUM_ZERO) ? kFlagAccumZero : 0u;
+    a.flags = ((desc->Flags & RT_FLAG_ACCUM_ZERO) ? kFlagAccumZero : 0u) |
+              ((desc->Flags & RT_FLAG_SRGB_POW) ? kFlagSrgbPow : 0u);
     a.band_rows = band_rows;
     a.band_count = band_count;
     a.band_index = desc->BandIndex;
@@ -829,6 +830,15 @@ extern "C" int rt_assemble_bands(const void *d_compact, uint64_t rank_stride_byt
     if (rtk_launch_assemble(d_compact, rank_stride_bytes, d_dst, width, height, elem_bytes, band_rows, band_count,
                             (hipStream_t)stream) != 0)
         return fail(RT_EIO, "rt_assemble_bands: launch failed");
+    return RT_OK;
+}
+
+extern "C" int rt_encode_rgba8(const float *d_accum_v4, uint32_t *d_rgba8, uint64_t n_pixels, uint32_t flags,
+                               void *stream) {
+    if ((!d_accum_v4 || !d_rgba8) && n_pixels) return fail(RT_EINVAL, "rt_encode_rgba8: NULL buffer");
+    if (flags & ~RT_FLAG_SRGB_POW) return fail(RT_EINVAL, "rt_encode_rgba8: unknown flags 0x%x", flags);
+    if (rtk_launch_encode(d_accum_v4, d_rgba8, n_pixels, (flags & RT_FLAG_SRGB_POW) ? 1u : 0u, (hipStream_t)stream) != 0)
+        return fail(RT_EIO, "rt_encode_rgba8: launch failed");
     return RT_OK;
 }
 

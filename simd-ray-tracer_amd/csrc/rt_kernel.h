@@ -10,7 +10,7 @@ constexpr uint32_t kGroupF4 = 5;      // float4 rows per sphere group:
 constexpr uint32_t kRowX = 0, kRowY = 1, kRowZ = 2;  //   centres
 constexpr uint32_t kRowR2P = 3;       //   prefilter thresholds (rows 0-3 = one s_load_dwordx16)
 constexpr uint32_t kRowR2 = 4;        //   r*r
-enum { kFlagAccumZero = 1 };
+enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
 // kClEntryF4 float4 rows, read through the scalar cache --
 //   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1} {b0 b1 0 0}
@@ -108,5 +108,6 @@ extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t
 // (dead pixels x frames) to the ray counter once.
 extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
                                 unsigned long long dead_rays, hipStream_t stream);
+extern "C" int rtk_launch_encode(const void *accum, void *out, uint64_t n, uint32_t pow_mode, hipStream_t stream);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

@@ -155,6 +155,30 @@ __device__ __forceinline__ float linear_to_srgb(float l) {  // main.cpp:312-329
     return l < 0.0031308f ? l * 12.92f : sqrt_rn(l);  // l in [0.0031308, 1]
 }
 
+// The exact-pow branch of LinearToSRGB (main.cpp:320-321, '#if 0' in the
+// reference; RT_FLAG_SRGB_POW).  powf there is libm's (musl in the WASM build,
+// glibc on Linux: the same algorithm, not correctly rounded); here the f64
+// pow rounded once to f32.  The two differ in the last f32 bit on ~46k of the
+// 70.4M inputs in [0.0031308, 1], and the RGBA8 byte on none of them
+// (exhaustive: tests/test_srgb_pow.py on the CPU, and the GPU's own bytes
+// against the oracle's over the same range in tests/test_gpu_parity.py).
+// Unfused, as wasm32 has no FMA.
+__device__ __forceinline__ float linear_to_srgb_pow(float l) {
+    l = saturate(l);
+    if (l < 0.0031308f) return l * 12.92f;
+    const float p = (float)pow((double)l, (double)(1.0f / 2.4f));
+    return 1.055f * p - 0.055f;
+}
+
+// ColorFromV4(LinearToSRGB(v)) (main.cpp:340-346, 490).
+__device__ __forceinline__ uint32_t rgba8(float x, float y, float z, bool pw) {
+    if (pw)
+        return to_u8(linear_to_srgb_pow(x)) | (to_u8(linear_to_srgb_pow(y)) << 8) |
+               (to_u8(linear_to_srgb_pow(z)) << 16) | (255u << 24);
+    return to_u8(linear_to_srgb(x)) | (to_u8(linear_to_srgb(y)) << 8) | (to_u8(linear_to_srgb(z)) << 16) |
+           (255u << 24);
+}
+
 __device__ __forceinline__ float reflectance(float cos_t, float eta) {  // main.cpp:292-300
     float r0 = (1.0f - eta) / (1.0f + eta);
     r0 *= r0;
@@ -1062,8 +1086,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     if (valid && owner && a.frames > 0) {
         const size_t pix = (size_t)ly * a.width + x;
         a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
-        a.cur[pix] = to_u8(linear_to_srgb(accx)) | (to_u8(linear_to_srgb(accy)) << 8) |
-                     (to_u8(linear_to_srgb(accz)) << 16) | (255u << 24);
+        a.cur[pix] = rgba8(accx, accy, accz, (a.flags & kFlagSrgbPow) != 0u);
     }
 
     // ---- ray counter (RaysCastInThread, main.cpp:390): one atomic per wave
@@ -1229,8 +1252,7 @@ __global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t 
         }
     }
     a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
-    a.cur[pix] = to_u8(linear_to_srgb(accx)) | (to_u8(linear_to_srgb(accy)) << 8) |
-                 (to_u8(linear_to_srgb(accz)) << 16) | (255u << 24);
+    a.cur[pix] = rgba8(accx, accy, accz, (a.flags & kFlagSrgbPow) != 0u);
 }
 
 // Scatter RCCL-gathered compact band images into the full framebuffer.
@@ -1488,6 +1510,26 @@ extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const u
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 #undef RTK_BY_P
+
+namespace rtk {
+// Re-encode a resident running mean (v4 f32) as RGBA8: the store of
+// main.cpp:490 on its own (rt_encode_rgba8).
+__global__ __launch_bounds__(256) void encode_kernel(const float4 *accum, uint32_t *out, uint64_t n, uint32_t pw) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const float4 v = accum[i];
+        out[i] = rgba8(v.x, v.y, v.z, pw != 0u);
+    }
+}
+}  // namespace rtk
+
+extern "C" int rtk_launch_encode(const void *accum, void *out, uint64_t n, uint32_t pow_mode, hipStream_t stream) {
+    if (n == 0) return 0;
+    const uint64_t blocks = (n + 255u) / 256u;
+    const uint32_t grid = (uint32_t)(blocks < 8192u ? blocks : 8192u);
+    hipLaunchKernelGGL(rtk::encode_kernel, dim3(grid), dim3(256), 0, stream, (const float4 *)accum, (uint32_t *)out, n,
+                       pow_mode);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream) {

@@ -28,7 +28,7 @@ def _scenes(rt, orc, index, n=None):
 
 
 def gpu_render(rt, torch, dev, scene, cam, W, H, *, frames, bounces, simd=True, prev_count=0, prev=None,
-               band_rows=32, band_count=1, band_index=0, accum_zero=False):
+               band_rows=32, band_count=1, band_index=0, accum_zero=False, srgb_pow=False):
     dev.upload_scene(scene)
     local = rt.band_local_rows(H, band_rows, band_count, band_index)
     if prev is None:
@@ -37,7 +37,7 @@ def gpu_render(rt, torch, dev, scene, cam, W, H, *, frames, bounces, simd=True, 
     rays = torch.zeros(1, dtype=torch.int64, device="cuda")
     dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
               prev_count=prev_count, frames=frames, max_bounce=bounces, simd=simd, band_rows=band_rows,
-              band_count=band_count, band_index=band_index, accum_zero=accum_zero,
+              band_count=band_count, band_index=band_index, accum_zero=accum_zero, srgb_pow=srgb_pow,
               stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     return prev, cur, int(rays.item())
@@ -372,3 +372,38 @@ def test_cull_masks_equal_cpu_restatement(rt, torch_cuda, monkeypatch, idx, n, W
         dev.close()
     ref = np_masks(rt, s, cam, W, H, P)
     assert got is not None and np.array_equal(got, ref), np.flatnonzero(got != ref)[:8]
+
+
+@pytest.mark.parametrize("simd", [True, False])
+def test_srgb_pow_flag_changes_only_the_rgba8(rt, orc, torch_cuda, gdev, simd):
+    """RT_FLAG_SRGB_POW (main.cpp:320-321): the running mean and ray count are
+    those of the default path; the RGBA8 is the oracle's pow-branch encoding."""
+    s, o = _scenes(rt, orc, 0)
+    W, H = 64, 48
+    cam = rt.camera_setup(s, W, H)
+    gp, gc, gr = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=3, bounces=5, simd=simd, srgb_pow=True)
+    op, oc, orays = orc.render(o, orc.camera(o, W, H), W, H, frames=3, max_bounce=5, simd=simd)
+    ocp = orc.encode_rgba8(op, srgb_pow=True)
+    assert not np.array_equal(ocp, oc.reshape(-1))
+    assert_same(gp, gc, gr, op, ocp, orays)
+
+
+def test_encode_rgba8_exhaustive(rt, orc, torch_cuda):
+    """rt_encode_rgba8 over every f32 the pow branch sees ([0.0031308, 1], three
+    per pixel) plus edge values, both curves: bytes equal the oracle's."""
+    torch = torch_cuda
+    lo = np.array([0.0031308], np.float32).view(np.uint32)[0]
+    vals = np.arange(lo, 0x3F800000 + 1, dtype=np.uint32).view(np.float32)
+    edge = np.array([-1.0, -0.0, 0.0, 1e-30, 0.001, 2.0, np.inf, -np.inf, np.nan], np.float32)
+    vals = np.concatenate([vals, edge, np.zeros((-(len(vals) + len(edge))) % 3, np.float32)])
+    v4 = np.ones((len(vals) // 3, 4), np.float32)
+    v4[:, :3] = vals.reshape(-1, 3)
+    d_in = torch.from_numpy(v4).cuda()
+    d_out = torch.zeros(len(v4), dtype=torch.int32, device="cuda")
+    for pw in (True, False):
+        rt.encode_rgba8(d_in.data_ptr(), d_out.data_ptr(), len(v4), srgb_pow=pw,
+                        stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = d_out.cpu().numpy().view(np.uint32)
+        want = orc.encode_rgba8(v4, srgb_pow=pw)
+        assert np.array_equal(got, want), f"pow={pw}: {int((got != want).sum())} pixels differ"
