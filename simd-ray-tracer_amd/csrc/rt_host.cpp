@@ -625,6 +625,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     if (!d->lut_set) return fail(RT_EINVAL, "rt_trace: rsqrt table not set (rt_set_rsqrt_table)");
     if (!d->scene_set) return fail(RT_EINVAL, "rt_trace: no scene uploaded (rt_scene_upload)");
     if (desc->SeedMode != RT_SEED_PIXEL) return fail(RT_EINVAL, "rt_trace: only RT_SEED_PIXEL runs on the GPU");
+    if (desc->Flags & ~(RT_FLAG_ACCUM_ZERO | RT_FLAG_SRGB_POW))
+        return fail(RT_EINVAL, "rt_trace: unknown Flags 0x%x", desc->Flags);
     if (desc->Width == 0 || desc->Height == 0 || desc->Width > 65536 || desc->Height > 65536)
         return fail(RT_EINVAL, "rt_trace: bad image size %ux%u", desc->Width, desc->Height);
     const uint32_t band_rows = desc->BandRows ? desc->BandRows : 32u;

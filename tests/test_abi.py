@@ -138,3 +138,6 @@ def test_trace_rejects_bad_arguments(rt):
     assert L.rt_scene_upload(None, None) == -22
     assert L.rt_assemble_bands(None, 0, None, 0, 0, 0, 0, 0, None) == -22
     assert b"bad argument" in L.rt_last_error()
+    assert L.rt_encode_rgba8(None, None, 1, 0, None) == -22
+    assert L.rt_encode_rgba8(None, None, 0, 4, None) == -22 and b"unknown flags" in L.rt_last_error()
+    assert L.rt_encode_rgba8(None, None, 0, rt.RT_FLAG_SRGB_POW, None) == 0  # nothing to encode: no launch
