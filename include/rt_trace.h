@@ -166,7 +166,9 @@ int rt_rsqrt_table_capture_host(float table_out[2048]);
 
 /* Uploads Scenes[SceneIndex] (read by RenderTile at main.cpp:370) into
  * HBM: SIMDSpheres/Materials for the SIMD rules, ScalarSpheres for the
- * scalar rules.  The scene is copied; the caller keeps ownership. */
+ * scalar rules.  The scene is copied; the caller keeps ownership.
+ * RT_EINVAL for a scene with no spheres (every built-in scene has some) or
+ * more than the LDS-staged limit (rt_kernel.h kMaxLdsGroups groups). */
 int rt_scene_upload(rt_device *dev, const rt_scene *scene);
 
 /* --------------------------------------------------------------- tracing */

@@ -141,3 +141,18 @@ def test_trace_rejects_bad_arguments(rt):
     assert L.rt_encode_rgba8(None, None, 1, 0, None) == -22
     assert L.rt_encode_rgba8(None, None, 0, 4, None) == -22 and b"unknown flags" in L.rt_last_error()
     assert L.rt_encode_rgba8(None, None, 0, rt.RT_FLAG_SRGB_POW, None) == 0  # nothing to encode: no launch
+
+
+def test_scene_size_limits(rt):
+    """rt_scene_upload's packer (shared with rt_scene_prefilter, no GPU needed)
+    rejects an empty scene and one past the LDS-staged limit (265 groups)."""
+    empty = rt.scene_from_spheres(np.zeros((0, 20), np.float32), use_sky=True)
+    with pytest.raises(rt.RtError, match="empty scene"):
+        rt.scene_prefilter(empty, True)
+    sp = np.zeros((4 * 265 + 1, 20), np.float32)
+    sp[:, 0] = np.arange(len(sp), dtype=np.float32)
+    sp[:, 4] = 0.25
+    with pytest.raises(rt.RtError, match="LDS-staged limit"):
+        rt.scene_prefilter(rt.scene_from_spheres(sp[:]), True)
+    r2, _, _ = rt.scene_prefilter(rt.scene_from_spheres(sp[:-1]), True)  # exactly at the limit
+    assert len(r2) == 4 * 265

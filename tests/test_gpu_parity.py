@@ -407,3 +407,30 @@ def test_encode_rgba8_exhaustive(rt, orc, torch_cuda):
         got = d_out.cpu().numpy().view(np.uint32)
         want = orc.encode_rgba8(v4, srgb_pow=pw)
         assert np.array_equal(got, want), f"pow={pw}: {int((got != want).sum())} pixels differ"
+
+
+def test_largest_scene_the_lds_image_holds(rt, orc, torch_cuda, gdev):
+    """1,060 spheres = 265 groups, the LDS-staged maximum (rt_kernel.h
+    kMaxLdsGroups): RTWeekend's 482 plus small spheres scattered over its
+    ground (their materials copied from RTWeekend's), both rule sets."""
+    base = rt.scene_builtin(2)
+    sp0, _, _ = rt.scene_arrays(base)
+    rng = np.random.default_rng(265)
+    extra = sp0[rng.integers(1, len(sp0), 4 * 265 - len(sp0))].copy()
+    extra[:, 0] = rng.uniform(-1.5, 1.5, len(extra))  # the scene is at 1/16 scale
+    extra[:, 2] = rng.uniform(-1.5, 1.5, len(extra))
+    extra[:, 4] = rng.uniform(0.005, 0.02, len(extra))
+    extra[:, 1] = extra[:, 4]
+    sp = np.concatenate([sp0, extra]).astype(np.float32)
+    la = (base.LookAt.x, base.LookAt.y, base.LookAt.z)
+    kw = dict(distance=base.DefaultDistanceFromLookAt, x_angle=base.DefaultXAngle, y_height=base.DefaultYHeight)
+    s = rt.scene_from_spheres(sp, look_at=la, use_sky=True, **kw)
+    _, groups, mats = rt.scene_arrays(s)
+    assert len(groups) == 265
+    o = orc.Scene(sp, groups, mats, look_at=la, use_sky=True, **kw)
+    W, H = 48, 32
+    cam = rt.camera_setup(s, W, H)
+    for simd in (True, False):
+        g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5, simd=simd)
+        r = orc.render(o, orc.camera(o, W, H), W, H, frames=2, max_bounce=5, simd=simd)
+        assert_same(*g, *r)
