@@ -211,6 +211,24 @@ uint32_t rt_band_local_rows(uint32_t height, uint32_t band_rows, uint32_t band_c
 int rt_trace(rt_device *dev, const rt_camera_info *cam, const rt_trace_desc *desc,
              uint64_t *d_rays, void *stream);
 
+/* What the last rt_trace on `dev` launched (host-side bookkeeping, no GPU
+ * synchronisation).  The reference counts every bounce segment, misses
+ * included (RaysCastInThread, main.cpp:390); segments of pixels whose every
+ * sample provably misses (no primary ray of their tile can reach a sphere,
+ * no sky term) are counted analytically and folded by a pixel kernel rather
+ * than traced: SegmentsFolded of the launch's ray count are such segments. */
+typedef struct rt_trace_info {
+    uint64_t SegmentsFolded;  /* dead-tile segments counted, not traced      */
+    uint32_t LanesPerPixel;   /* P of the launch (sample chains per pixel)   */
+    uint32_t TilesTotal;      /* block tiles of the band geometry            */
+    uint32_t TilesTraced;     /* live tiles launched on the trace kernel     */
+    uint32_t CullPassRan;     /* 1: this launch ran the primary-ray cull pass */
+    uint32_t OrderedLaunches; /* heaviest-first re-sorts done for this key   */
+    uint32_t ClusteredWalk;   /* 1: secondary rays used the cluster walk     */
+    uint32_t GroupsPerRuleSet;/* sphere groups of the rule set traced        */
+} rt_trace_info;
+int rt_trace_last_info(rt_device *dev, rt_trace_info *out);
+
 /* ColorFromV4(LinearToSRGB(v)) (main.cpp:312-346, the store at :490) over a
  * device-resident running mean: n_pixels v4 f32 -> RGBA8, both DEVICE
  * pointers, enqueued on `stream` (NULL: the null stream).  flags: 0 or

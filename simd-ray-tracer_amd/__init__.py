@@ -87,6 +87,12 @@ class RtTraceDesc(ctypes.Structure):
                                         "SeedMode", "BandRows", "BandCount", "BandIndex", "Flags")]
 
 
+class RtTraceInfo(ctypes.Structure):  # rt_trace_last_info
+    _fields_ = [("SegmentsFolded", c_uint64)] + [(n, c_uint32) for n in (
+        "LanesPerPixel", "TilesTotal", "TilesTraced", "CullPassRan", "OrderedLaunches", "ClusteredWalk",
+        "GroupsPerRuleSet")]
+
+
 for _t, _n in ((RtV3, 16), (RtMaterial, 48), (RtScalarSphere, 80), (RtSphereGroup, 64), (RtArray, 16),
                (RtScene, 80), (RtImage, 24), (RtCameraInfo, 144), (RtRenderParams, 12)):
     assert ctypes.sizeof(_t) == _n, (_t.__name__, ctypes.sizeof(_t), _n)
@@ -108,6 +114,7 @@ SIGNATURES = {
     "rt_trace": (c_int, [c_void_p, POINTER(RtCameraInfo), POINTER(RtTraceDesc), c_void_p, c_void_p]),
     "rt_assemble_bands": (c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
                                   c_void_p]),
+    "rt_trace_last_info": (c_int, [c_void_p, POINTER(RtTraceInfo)]),
     "rt_encode_rgba8": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "rt_device_synchronize": (c_int, [c_void_p]),
     "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
@@ -297,6 +304,14 @@ class Device:
                         (RT_FLAG_ACCUM_ZERO if accum_zero else 0) | (RT_FLAG_SRGB_POW if srgb_pow else 0))
         _check(lib().rt_trace(self.handle, ctypes.byref(c), ctypes.byref(d), c_void_p(rays_ptr),
                               c_void_p(stream or 0)), "rt_trace")
+
+    def last_info(self) -> dict:
+        """What the last trace launched (rt_trace_last_info): segments counted
+        but folded analytically (dead tiles), P, tiles traced / total, whether
+        the cull pass ran."""
+        info = RtTraceInfo()
+        _check(lib().rt_trace_last_info(self.handle, ctypes.byref(info)), "rt_trace_last_info")
+        return {n: int(getattr(info, n)) for n, _ in RtTraceInfo._fields_}
 
     def debug_stats(self, reset: bool = True):
         """RT_STATS=1 scheduling counters (see rt_debug_stats), or None when disabled."""

@@ -68,6 +68,7 @@ struct rt_device {
     unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
     size_t wave_times_cap = 0;
     bool want_wave_times = false;
+    rt_trace_info last{};  // what the last rt_trace launched (rt_trace_last_info)
 };
 
 static thread_local char g_err[512];
@@ -161,9 +162,20 @@ extern "C" int rt_device_destroy(rt_device *d) {
     return RT_OK;
 }
 
+// rt_trace is asynchronous on the caller's stream (d->tile_stream), while
+// uploads go through the device's own non-blocking stream: before a buffer a
+// trace may still read (scene groups, materials, cluster table, rsqrt table)
+// is overwritten, every launch issued so far must have finished.
+static int quiesce(rt_device *d) {
+    if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(d->tile_stream));
+    HIP_OK(hipStreamSynchronize(d->stream));
+    return RT_OK;
+}
+
 extern "C" int rt_set_rsqrt_table(rt_device *d, const float table[2048]) {
     if (!d || !table) return fail(RT_EINVAL, "rt_set_rsqrt_table: NULL argument");
     HIP_OK(hipSetDevice(d->ordinal));
+    if (const int rc = quiesce(d)) return rc;
     HIP_OK(hipMemcpyAsync(d->d_lut, table, 2048 * sizeof(float), hipMemcpyHostToDevice, d->stream));
     HIP_OK(hipStreamSynchronize(d->stream));
     d->lut_set = true;
@@ -554,6 +566,7 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
         if (rc) return rc;
     }
     HIP_OK(hipSetDevice(d->ordinal));
+    if (const int rc = quiesce(d)) return rc;
     for (int rs = 0; rs < 2; ++rs) {
         d->prefilter[rs] = d->prefilter_env < 0 ? (ps[rs].prefilter_pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
         d->fast_sqrt[rs] = ps[rs].fast_sqrt;
@@ -773,7 +786,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         d->mask_cap = mask_words;
         d->tile_key.clear();
     }
-    if (key != d->tile_key) {
+    const bool new_key = key != d->tile_key;
+    if (new_key) {
         d->tile_key = key;
         d->n_sorts = 0;
         if (cull) {
@@ -803,6 +817,14 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.masks = cull ? d->d_masks : nullptr;
     a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
     a.tile_cost = sched ? d->d_tile_cost : nullptr;
+    d->last.SegmentsFolded = empty_capable && d->n_live < n_tiles ? d->dead_pixels * desc->Frames : 0u;
+    d->last.LanesPerPixel = (uint32_t)lpp;
+    d->last.TilesTotal = n_tiles;
+    d->last.TilesTraced = d->n_live;
+    d->last.CullPassRan = cull && new_key ? 1u : 0u;
+    d->last.OrderedLaunches = d->n_sorts;
+    d->last.ClusteredWalk = a.clusters ? 1u : 0u;
+    d->last.GroupsPerRuleSet = a.n_groups;
     if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, d->src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (empty_capable && d->n_live < n_tiles &&
@@ -844,11 +866,16 @@ extern "C" int rt_encode_rgba8(const float *d_accum_v4, uint32_t *d_rgba8, uint6
     return RT_OK;
 }
 
+extern "C" int rt_trace_last_info(rt_device *d, rt_trace_info *out) {
+    if (!d || !out) return fail(RT_EINVAL, "rt_trace_last_info: NULL argument");
+    *out = d->last;
+    return RT_OK;
+}
+
 extern "C" int rt_device_synchronize(rt_device *d) {
     if (!d) return fail(RT_EINVAL, "rt_device_synchronize: NULL device");
     HIP_OK(hipSetDevice(d->ordinal));
-    HIP_OK(hipStreamSynchronize(d->stream));
-    return RT_OK;
+    return quiesce(d);
 }
 
 extern "C" int rt_debug_stats(rt_device *d, uint64_t out[32], int reset) {

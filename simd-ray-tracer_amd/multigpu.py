@@ -1,12 +1,13 @@
 """Per-GPU band dispatch and the rank-0 gather.
 
-The image is cut into 32-row bands (the reference's TileSize, main.cpp:9)
-dealt round-robin to the ranks: band b -> rank b % world.  Each rank traces
-its bands into a compact local image (rt_band_local_rows x W), pads it to the
-largest rank's size, and one collective gather (RCCL over xGMI on the GPU,
-gloo in the CPU tests) brings every rank's buffer to rank 0, which scatters
-the bands back into place (rt_assemble_bands on the GPU).  Samples are never
-split across ranks: the running-mean fold is order dependent (main.cpp:487).
+The image is cut into row bands (bench.py uses 8 rows; the tests also use
+the reference's 32-row TileSize, main.cpp:9) dealt round-robin to the
+ranks: band b -> rank b % world.  Each rank traces its bands into a compact
+local image (rt_band_local_rows x W), pads it to the largest rank's size,
+and one collective gather (RCCL over xGMI on the GPU, gloo in the CPU tests)
+brings every rank's buffer to rank 0, which scatters the bands back into
+place (rt_assemble_bands on the GPU).  Samples are never split across
+ranks: the running-mean fold is order dependent (main.cpp:487).
 """
 from __future__ import annotations
 

@@ -225,10 +225,12 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
 
 
 # Kernel variants selected at device creation (rt_host.cpp reads the env):
-# prefilter forced on/off, brute-force primaries, 1/2 lanes per pixel.  Every
-# variant must give the same bits as the oracle.
-VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"}, {"RT_INTERLEAVE": "1"}, {"RT_CULL": "0"},
-                {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"}, {"RT_SEC_THRESHOLD": "1"}]
+# prefilter forced on/off, brute-force primaries, 1/2/32 lanes per pixel, the
+# LDS-staged sphere source.  Every variant must give the same bits as the oracle.
+VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"},
+                {"RT_INTERLEAVE": "1"}, {"RT_CULL": "0"}, {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"},
+                {"RT_LANES_PER_PIXEL": "32"}, {"RT_SEC_THRESHOLD": "1"}, {"RT_SPHERE_SRC": "lds"},
+                {"RT_SPHERE_SRC": "lds", "RT_CULL": "0"}, {"RT_SPHERE_SRC": "lds", "RT_CLUSTERS": "0"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
@@ -434,3 +436,45 @@ def test_largest_scene_the_lds_image_holds(rt, orc, torch_cuda, gdev):
         g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5, simd=simd)
         r = orc.render(o, orc.camera(o, W, H), W, H, frames=2, max_bounce=5, simd=simd)
         assert_same(*g, *r)
+
+
+def test_upload_waits_for_traces_in_flight(rt, orc, torch_cuda):
+    """rt_trace is asynchronous on the caller's stream; rt_scene_upload writes
+    through the device's own stream.  Uploading scene B right after enqueueing
+    a trace of scene A (no synchronisation in between, same allocation size)
+    must not change A's frame: both frames equal the oracle's."""
+    torch = torch_cuda
+    sa, oa = _scenes(rt, orc, 1, 64)
+    spb, _, _ = rt.scene_arrays(sa)
+    spb = spb.copy()
+    spb[:, 1] += np.float32(0.05)  # same sphere count, every centre moved
+    sb = rt.scene_from_spheres(spb, look_at=(sa.LookAt.x, sa.LookAt.y, sa.LookAt.z),
+                               distance=sa.DefaultDistanceFromLookAt, x_angle=sa.DefaultXAngle,
+                               y_height=sa.DefaultYHeight)
+    _, gb, mb = rt.scene_arrays(sb)
+    ob = orc.Scene(spb, gb, mb, look_at=(sa.LookAt.x, sa.LookAt.y, sa.LookAt.z), distance=sa.DefaultDistanceFromLookAt,
+                   x_angle=sa.DefaultXAngle, y_height=sa.DefaultYHeight)
+    W, H, S, B = 320, 240, 16, 8
+    cam = rt.camera_setup(sa, W, H)
+    dev = rt.Device(0)
+    side = torch.cuda.Stream()
+    try:
+        out = []
+        dev.upload_scene(sa)
+        for scene in (sb, None):
+            prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            with torch.cuda.stream(side):
+                dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                          rays_ptr=rays.data_ptr(), frames=S, max_bounce=B, stream=side.cuda_stream)
+            if scene is not None:
+                dev.upload_scene(scene)  # no synchronisation with `side` by the caller
+            side.synchronize()
+            out.append((prev, cur, int(rays.item())))
+    finally:
+        dev.close()
+    for (p, c, n), o in zip(out, (oa, ob)):
+        r = orc.render(o, orc.camera(o, W, H), W, H, frames=S, max_bounce=B)
+        assert_same(p, c, n, *r)
