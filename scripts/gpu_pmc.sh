@@ -1,13 +1,19 @@
-# PMC passes over one bench launch (kernel-trace counters only, no sys-trace).
+# PMC passes over the trace kernel (kernel-trace counters only, no sys-trace):
+# bench.py --steps 1 --warmup 3 under each counter set; scripts/pmc_to_json.py
+# keeps the LAST trace_kernel dispatch of every pass (the warm launch the
+# bench times, learned tile order in place).
 # usage: bash scripts/gpu_pmc.sh <tag> [extra bench args]
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 tag=$1; shift
 i=0
-for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32 SQ_WAVES GRBM_GUI_ACTIVE" "SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_IFETCH SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32" "FETCH_SIZE" "WRITE_SIZE"; do
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_ACTIVE_INST_VALU2 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" \
+           "SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_IFETCH GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set -d gpurun_out/pmc_${tag}_$i -o p --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > gpurun_out/pmc_${tag}_$i.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $set -d gpurun_out/pmc_${tag}_$i -o p --output-format csv -- python bench.py --steps 1 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/pmc_${tag}_$i.log 2>&1 || { tail -5 gpurun_out/pmc_${tag}_$i.log; exit 1; }
 done
-python scripts/pmc_summary.py gpurun_out pmc_${tag}_ > gpurun_out/pmc_${tag}_summary.txt
-cat gpurun_out/pmc_${tag}_summary.txt
+echo "pmc passes done: $i"
