@@ -33,6 +33,10 @@ sys.path.insert(0, str(ROOT))
 # HBM3E 8 TB/s.
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
+SIMDS = 256 * 4
+# the verbatim reference, one thread, N=64, 8 bounces, pixel
+# seeds, measured on the survey host: about 11-12.5 Mrays/s per core.
+REF_SINGLE_THREAD_MRAYS = (11.0, 12.5)
 
 
 def ops_per_segment(n_spheres: int) -> int:
@@ -43,11 +47,18 @@ def ops_per_segment(n_spheres: int) -> int:
 # BASELINE.json configs: C2 is the headline (1 GPU) and the
 # default; C4 is C2 on several GPUs; C3 / C5 are the large single- and
 # multi-GPU cases.  C1 is the CPU-only plumbing case (tests, not a bench line).
+# "rtw" and "c2in" are frames the primary-ray cull cannot empty:
+# RTWeekend (main.cpp:193-268, 482 spheres, sky term: every pixel is traced)
+# and C2's 64 spheres seen from inside the sphere cloud (camera 1.0 from the
+# look-at point instead of 3.0).
 CONFIGS = {
-    "c2": dict(width=1920, height=1080, spp=256, spheres=64, bounces=8),
-    "c3": dict(width=3840, height=2160, spp=1024, spheres=64, bounces=8),
-    "c5": dict(width=7680, height=4320, spp=4096, spheres=256, bounces=16),
+    "c2": dict(width=1920, height=1080, spp=256, spheres=64, bounces=8, scene=1, distance=None),
+    "c3": dict(width=3840, height=2160, spp=1024, spheres=64, bounces=8, scene=1, distance=None),
+    "c5": dict(width=7680, height=4320, spp=4096, spheres=256, bounces=16, scene=1, distance=None),
+    "rtw": dict(width=1920, height=1080, spp=64, spheres=482, bounces=8, scene=2, distance=None),
+    "c2in": dict(width=1920, height=1080, spp=256, spheres=64, bounces=8, scene=1, distance=1.0),
 }
+SCENE_NAMES = {0: "RGB Glass", 1: "Floating Spheres", 2: "RTWeekend"}
 
 
 def parse():
@@ -61,6 +72,8 @@ def parse():
     p.add_argument("--spp", type=int)
     p.add_argument("--spheres", type=int)
     p.add_argument("--bounces", type=int)
+    p.add_argument("--scene", type=int, choices=(0, 1, 2), help="built-in scene (default: the config's)")
+    p.add_argument("--distance", type=float, help="camera distance from the look-at point (default: the scene's)")
     p.add_argument("--scalar", action="store_true", help="RenderTileScalar rules instead of RenderTile")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -79,6 +92,15 @@ def parse():
     return a
 
 
+def make_scene(rt, args):
+    """The workload's scene: the first `spheres` spheres of a built-in scene."""
+    scene = rt.scene_builtin(args.scene)
+    if args.spheres < scene.ScalarSpheres.Count:
+        scene = rt.scene_prefix(scene, args.spheres)
+    args.spheres = scene.ScalarSpheres.Count
+    return scene
+
+
 def cpu_baseline(args, n_rays_gpu_step: int):
     """The oracle (C restatement of RenderTile, lane-4 SSE, pthread 32x32 tile
     queue) on this host's cores, on a bounded sample of the same workload:
@@ -89,9 +111,11 @@ def cpu_baseline(args, n_rays_gpu_step: int):
     env_cap = os.environ.get("OMP_NUM_THREADS")
     if env_cap and env_cap.isdigit():
         threads = min(threads, int(env_cap))
-    o = orc.scene_builtin(1).prefix(args.spheres)
+    o = orc.scene_builtin(args.scene)
+    if args.spheres < len(o.spheres):
+        o = o.prefix(args.spheres)
     W, H = args.width, args.height
-    cam = orc.camera(o, W, H)
+    cam = orc.camera(o, W, H, distance=args.distance)
     t = time.perf_counter()
     _, _, rays1 = orc.render(o, cam, W, H, frames=1, max_bounce=args.bounces, threads=threads, simd=not args.scalar)
     dt1 = time.perf_counter() - t
@@ -99,23 +123,37 @@ def cpu_baseline(args, n_rays_gpu_step: int):
     t = time.perf_counter()
     _, _, rays = orc.render(o, cam, W, H, frames=k, max_bounce=args.bounces, threads=threads, simd=not args.scalar)
     dt = time.perf_counter() - t
+    # the port counts as the reference's speed only if its single-thread
+    # rate is within +-10 % of the verbatim reference's on the probe workload
+    # (480x270, 8 spp, N = 64, 8 bounces, one thread: ~11-12.5 Mrays/s on the survey host)
+    p = orc.scene_builtin(1).prefix(64)
+    pc = orc.camera(p, 480, 270)
+    t = time.perf_counter()
+    _, _, prays = orc.render(p, pc, 480, 270, frames=8, max_bounce=8, threads=1)
+    pdt = time.perf_counter() - t
+    single = prays / pdt / 1e6
+    lo, hi = REF_SINGLE_THREAD_MRAYS
     return {"value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{W}x{H}, {k} spp (of {args.spp}), {args.spheres} spheres, {args.bounces} bounces, "
                       f"{rays} rays in {dt:.2f} s on {threads} threads (oracle/rt_oracle.c, lane-4 SSE "
-                      f"RenderTile restatement, pixel seeds)"}
+                      f"RenderTile restatement, pixel seeds)",
+            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "single_thread": {"value": round(single, 2), "unit": "Mrays/s",
+                              "sample": f"480x270, 8 spp, 64 spheres, 8 bounces, 1 thread, {prays} rays in "
+                                        f"{pdt:.2f} s (SURVEY 8d calibration workload)",
+                              "reference_single_thread": [lo, hi],
+                              "ratio_to_reference": round(single / ((lo + hi) / 2), 3),
+                              "within_10pct": bool(0.9 * lo <= single <= 1.1 * hi)}}
 
 
-def lanes_per_pixel(band_pixels: int, frames: int) -> int:
-    """The P rt_trace picks for a band (rt_host.cpp rt_trace; RT_LANES_PER_PIXEL overrides), for the line's label."""
-    import torch
-    forced = os.environ.get("RT_LANES_PER_PIXEL")
-    if forced in ("1", "2", "4", "8", "16", "32"):
-        return int(forced)
-    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    p = 4 if band_pixels >= cus * 6144 else 8 if band_pixels >= cus * 1536 else 16
-    while p > 1 and p // 2 >= frames:
-        p //= 2
-    return p
+def cpu_model() -> str:
+    try:
+        for line in pathlib.Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def pmc_record(workload: str):
@@ -130,6 +168,36 @@ def pmc_record(workload: str):
             rec["file"] = f"profiles/{f.name}"
             return rec
     return None
+
+
+def valu_roofline(pmc, kern_ms: float):
+    """Executed-work roofline of the trace kernel from its committed PMC record
+    (scripts/gpu_pmc.sh -> scripts/pmc_to_json.py, the warm dispatch).
+
+    gfx950 VALU issue, calibrated on scripts/mb_ops (profiles/r02_pmc_calib.txt):
+    SQ_ACTIVE_INST_VALU counts one quad-cycle per wave64 VALU instruction (two
+    for transcendentals); full-rate ops (f32 add/mul/fma, 32-bit logic) can
+    pair, and SQ_ACTIVE_INST_VALU2 counts the quad-cycles in which two issued.
+    So a SIMD's VALU is occupied for ACTIVE_INST_VALU - ACTIVE_INST_VALU2
+    quad-cycles, out of cycles/4:
+        frac = (ACTIVE_INST_VALU - ACTIVE_INST_VALU2) / (1024 SIMDs x cycles / 4)
+    (<= 1: a VALU-bound kernel reaches 1 when every SIMD issues every
+    quad-cycle).  One quad-cycle slot is the capacity of 128 f32 add/mul lane
+    ops (a dual-issued wave64 pair, or one v_pk_*_f32), so `achieved` =
+    slots x 128 / live kernel time is in f32 add/mul-equivalent TFLOP/s
+    against the 78.6 T peak."""
+    c = pmc["counters_per_dispatch"]
+    cycles = pmc["gpu_cycles_per_dispatch"]
+    slots = c["SQ_ACTIVE_INST_VALU"] - c["SQ_ACTIVE_INST_VALU2"]
+    frac = slots / (SIMDS * cycles / 4.0)
+    return {"frac": round(frac, 4), "achieved": round(slots * 128 / (kern_ms / 1e3) / 1e12, 2),
+            "valu_slots_per_launch": slots,
+            "valu_instructions_per_launch": c["SQ_INSTS_VALU"],
+            "dual_issue_share": round(2 * c["SQ_ACTIVE_INST_VALU2"] / c["SQ_ACTIVE_INST_VALU"], 4),
+            "lane_utilisation": round(c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"]), 4),
+            "wave_cycles_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4),
+            "salu_per_valu": round(c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"], 4),
+            "gpu_cycles_per_launch": cycles}
 
 
 def main():
@@ -156,9 +224,9 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    scene = make_scene(rt, args)
     W, H, S, B, N = args.width, args.height, args.spp, args.bounces, args.spheres
-    scene = rt.scene_prefix(rt.scene_builtin(1), N)
-    cam = rt.camera_setup(scene, W, H)
+    cam = rt.camera_setup(scene, W, H, distance=args.distance)
     dev = rt.Device(gpu)
     dev.upload_scene(scene)
     band_rows = args.band_rows
@@ -211,11 +279,30 @@ def main():
             finish()
             state["pending"] = (work, slot)
 
-    for _ in range(max(args.warmup, 1)):
+    # Cold launch: the first launch for this camera / scene / geometry runs the
+    # primary-ray cull pass and traces in the cull pass's live-first tile order
+    # (the heaviest-first order is learned over the next launches).  A tiny
+    # launch first loads the code objects, so cold_ms is the render's own cost.
+    tiny_prev = torch.zeros((64 * 8, 4), dtype=torch.float32, device="cuda")
+    tiny_cur = torch.zeros(64 * 8, dtype=torch.int32, device="cuda")
+    dev.trace(cam, width=64, height=8, prev_ptr=tiny_prev.data_ptr(), cur_ptr=tiny_cur.data_ptr(),
+              rays_ptr=rays.data_ptr(), frames=1, max_bounce=1, simd=not args.scalar, band_rows=8,
+              accum_zero=True, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    step()
+    finish()
+    torch.cuda.synchronize()
+    cold_ms = (time.perf_counter() - t) * 1e3
+    cold_info = dev.last_info()
+    for _ in range(max(args.warmup - 1, 0)):
         step()
     finish()
     torch.cuda.synchronize()
-    rays_per_step = torch.tensor([int(rays.item())], dtype=torch.int64, device="cuda")
+    rays_per_step = torch.tensor([int(rays.item()), dev.last_info()["SegmentsFolded"]], dtype=torch.int64,
+                                 device="cuda")
     if world > 1:
         dist.all_reduce(rays_per_step)
         dist.barrier()
@@ -228,6 +315,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    info = dev.last_info()
     verified = None
     if args.verify and bands == world:  # rank 0 renders the whole frame alone and compares
         if rank == 0:
@@ -243,46 +331,53 @@ def main():
         if world > 1:
             dist.barrier()
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed, kern_ms, cold_ms], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms_max = float(t[0]), float(t[1])
-    total_rays = int(rays_per_step.item()) * args.steps
+    elapsed, kern_ms_max, cold_ms = float(t[0]), float(t[1]), float(t[2])
+    seg_counted, seg_folded = int(rays_per_step[0].item()), int(rays_per_step[1].item())
+    total_rays = seg_counted * args.steps
     value = total_rays / elapsed / 1e6
 
     if bands != world:
         if rank == 0:
             print(json.dumps({"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
-                              "rank0_kernel_ms": round(kern_ms, 3),
+                              "rank0_kernel_ms": round(kern_ms, 3), "lanes_per_pixel": info["LanesPerPixel"],
                               "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}))
         dev.close()
         return
     if rank == 0:
         rays_local = int(rays.item())  # rank 0's rays per launch
         ops = rays_local * ops_per_segment(N)
-        achieved = ops / (kern_ms / 1e3) / 1e12
+        achieved_alg = ops / (kern_ms / 1e3) / 1e12
         fb_bytes = rows[0] * W * (16 + 4)  # accumulation + RGBA8 written once per launch
         hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
         preset = all(getattr(args, k) == v for k, v in CONFIGS[args.config].items())
         tag = args.config.upper() if preset else "custom"
-        workload = f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
+        view = "" if args.distance is None else f", camera {args.distance:g} from look-at"
+        workload = (f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
+                    + ("" if args.scene == 1 else f", {SCENE_NAMES[args.scene]}") + view)
         pmc = pmc_record(workload)
-        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 1),
-                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
-                "traffic": round(pmc["hbm_bytes_per_dispatch"]) if pmc and "hbm_bytes_per_dispatch" in pmc else None,
-                "kernel": f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{lanes_per_pixel(rows[0] * W, S)}>",
-                "kernel_ms": round(kern_ms, 3),
-                "work_per_launch": f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d, brute force)",
-                "note": "algorithmic ops count every sphere for every segment; the kernel culls sphere groups "
-                        "for primary rays exactly, so it executes fewer ops and frac may exceed 1. The "
-                        "executed-instruction view is 'issue' (PMC).",
-                "hbm": {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}}
+        kernel = f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{info['LanesPerPixel']}>"
+        roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1), "unit": "TFLOP/s",
+                "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": round(kern_ms, 3)}
         if pmc:
-            roof["issue"] = {k: round(pmc[k], 4) for k in ("valu_inst_per_simd_cycle", "valu_lane_utilisation") if k in pmc}
-            roof["issue"]["ceiling"] = "0.5 full-rate / 0.25 half-rate (v_pk_*, int mul) wave-instr per SIMD-cycle"
-            roof["issue"]["source"] = pmc["file"]
-            roof["traffic_source"] = pmc["file"] + " (FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+            ex = valu_roofline(pmc, kern_ms)
+            roof["achieved"], roof["frac"] = ex.pop("achieved"), ex.pop("frac")
+            roof["traffic"] = round(pmc["hbm_bytes_per_dispatch"]) if "hbm_bytes_per_dispatch" in pmc else None
+            roof["executed"] = ex
+            roof["source"] = pmc["file"]
+            roof["note"] = ("frac = VALU issue occupancy of the trace kernel from the committed PMC record: "
+                            "(SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4); "
+                            "achieved = those quad-cycle slots x 128 f32 lane-ops / live kernel ms "
+                            "(bench.py valu_roofline). traffic = FETCH_SIZE x2 + WRITE_SIZE (KiB), per launch.")
+        roof["frac_algorithmic"] = round(achieved_alg / VALU_PEAK_TOPS, 4)
+        roof["achieved_algorithmic"] = round(achieved_alg, 2)
+        roof["work_per_launch"] = (f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d brute force; the "
+                                   "kernel skips most sphere tests exactly, so this rate can exceed the peak)")
+        roof["hbm"] = {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}
+        seg_traced = seg_counted - seg_folded
         line = {
             "metric": f"Mrays/sec at {W}x{H}, {S}spp, {B} bounces, {N} spheres",
             "value": round(value, 1),
@@ -295,13 +390,25 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic (first {N} spheres of the reference's Floating Spheres scene, default camera, "
-                    "per-(pixel,frame) PCG seeds)",
+            "data": f"synthetic ({'first ' + str(N) + ' spheres of ' if args.scene == 1 else ''}the reference's "
+                    f"{SCENE_NAMES[args.scene]} scene, {'default camera' if args.distance is None else 'camera moved'}"
+                    ", per-(pixel,frame) PCG seeds)",
             "config": {"workload": workload,
-                       "width": W, "height": H, "spp": S, "spheres": N, "bounces": B,
+                       "width": W, "height": H, "spp": S, "spheres": N, "bounces": B, "scene": args.scene,
                        "parallelism": f"{world} GPU x interleaved {band_rows}-row bands" +
                                       (" + RCCL gather" if world > 1 else ""),
-                       "rays_per_step": int(rays_per_step.item())},
+                       "rays_per_step": seg_counted},
+            "segments": {"counted_per_step": seg_counted, "traced_per_step": seg_traced,
+                         "folded_per_step": seg_folded,
+                         "traced_mrays_per_s": round(seg_traced * args.steps / elapsed / 1e6, 1),
+                         "note": "every segment is counted as the reference counts it (main.cpp:390); 'folded' "
+                                 "ones belong to pixels whose every sample provably misses (dead tiles), folded "
+                                 "by the empty-tile kernel instead of traced"},
+            "cold_ms": round(cold_ms, 3),
+            "cold": {"ms": round(cold_ms, 3), "cull_pass": bool(cold_info["CullPassRan"]),
+                     "note": "first launch for this camera/scene/geometry (cull pass + untrained tile order), "
+                             "wall clock incl. its host synchronisation; the timed steps reuse the cull masks "
+                             "and the learned heaviest-first order"},
             "roofline": roof,
         }
         stats = dev.debug_stats()
