@@ -234,19 +234,46 @@ def main():
     rows = [rt.band_local_rows(H, band_rows, bands, r) for r in range(bands)]
     maxr = max(rows)
     band_index = args.sim_index if bands != world else rank
-    # Two frame slots: frame i's band image is gathered to rank 0 (RCCL, async)
-    # while frame i+1 is traced; rank 0 assembles frame i before frame i+2
-    # reuses its slot.  The timed region ends only after the last frame is
-    # assembled on rank 0.
+    # Two frame slots: frame i's band image is gathered to rank 0 while frame
+    # i+1 is traced; rank 0 assembles frame i before frame i+2 reuses its slot.
+    # The gather is the C-ABI's RCCL band gather (rt_comm_gather_bands: grouped
+    # send/recv to rank 0 over xGMI, then the scatter into the full frame) on a
+    # side stream; a rehearsal with every rank on one GPU (BENCH_SHARE_GPU=1,
+    # which RCCL refuses) uses a torch.distributed gather.  The timed region
+    # ends only after the last frame is assembled on rank 0.
     cur = [torch.zeros(maxr * W, dtype=torch.int32, device="cuda") for _ in range(2)]
     prev = torch.zeros((maxr * W, 4), dtype=torch.float32, device="cuda")
     rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream()
+    comm, gather_kind = None, None
+    if world > 1:
+        gather_kind = f"torch.distributed {backend} gather + rt_assemble_bands"
+        if backend == "nccl" and os.environ.get("BENCH_SHARE_GPU") != "1":
+            uid = [rt.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            err = ""
+            try:
+                comm = rt.Comm(gpu, uid[0], world, rank)
+            except rt.RtError as e:
+                err = str(e)
+            ok = torch.tensor([1 if comm else 0], dtype=torch.int32, device="cuda")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 1:
+                gather_kind = "RCCL grouped send/recv to rank 0 + scatter (rt_comm_gather_bands)"
+            else:
+                if comm:
+                    comm.close()
+                comm = None
+                gather_kind += f" (rt_comm unavailable: {err or 'on another rank'})"
+                print(f"bench.py: {gather_kind}", file=sys.stderr)
     gbuf = full = None
     if world > 1 and rank == 0:
-        gdev = "cuda" if backend == "nccl" else "cpu"
-        gbuf = [torch.empty((world, maxr * W), dtype=torch.int32, device=gdev) for _ in range(2)]
         full = torch.empty(H * W, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream()
+        if comm is None:
+            gdev = "cuda" if backend == "nccl" else "cpu"
+            gbuf = [torch.empty((world, maxr * W), dtype=torch.int32, device=gdev) for _ in range(2)]
+    side = torch.cuda.Stream() if comm else None
+    gathered = [None, None]  # per slot: event after its gather on the side stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     state = {"n": 0, "pending": None}
 
@@ -264,6 +291,8 @@ def main():
     def step(i=None):
         slot = state["n"] % 2
         state["n"] += 1
+        if gathered[slot] is not None:  # the gather two frames back has read this slot
+            stream.wait_event(gathered[slot])
         rays.zero_()
         if i is not None:
             ev[i][0].record(stream)
@@ -273,7 +302,15 @@ def main():
                   stream=stream.cuda_stream)
         if i is not None:
             ev[i][1].record(stream)
-        if world > 1:  # RCCL gather of the band images to rank 0 over xGMI, then assembly
+        if world > 1 and comm is not None:
+            traced = torch.cuda.Event()
+            traced.record(stream)
+            side.wait_event(traced)
+            comm.gather_bands(cur[slot].data_ptr(), full.data_ptr() if rank == 0 else 0, W, H, 4, band_rows,
+                              stream=side.cuda_stream)
+            gathered[slot] = torch.cuda.Event()
+            gathered[slot].record(side)
+        elif world > 1:
             send = cur[slot] if backend == "nccl" else cur[slot].cpu()
             work = dist.gather(send, list(gbuf[slot].unbind(0)) if rank == 0 else None, dst=0, async_op=True)
             finish()
@@ -344,6 +381,8 @@ def main():
             print(json.dumps({"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
                               "rank0_kernel_ms": round(kern_ms, 3), "lanes_per_pixel": info["LanesPerPixel"],
                               "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}))
+        if comm:
+            comm.close()
         dev.close()
         return
     if rank == 0:
@@ -395,8 +434,8 @@ def main():
                     ", per-(pixel,frame) PCG seeds)",
             "config": {"workload": workload,
                        "width": W, "height": H, "spp": S, "spheres": N, "bounces": B, "scene": args.scene,
-                       "parallelism": f"{world} GPU x interleaved {band_rows}-row bands" +
-                                      (" + RCCL gather" if world > 1 else ""),
+                       "parallelism": f"{world} GPU x interleaved {band_rows}-row bands",
+                       **({"gather": gather_kind} if world > 1 else {}),
                        "rays_per_step": seg_counted},
             "segments": {"counted_per_step": seg_counted, "traced_per_step": seg_traced,
                          "folded_per_step": seg_folded,
@@ -419,6 +458,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, total_rays)
         print(json.dumps(line), flush=True)
+    if comm:
+        comm.close()
     dev.close()
     if world > 1:
         dist.destroy_process_group()

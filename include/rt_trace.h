@@ -246,6 +246,80 @@ int rt_assemble_bands(const void *d_compact, uint64_t rank_stride_bytes, void *d
 
 int rt_device_synchronize(rt_device *dev);
 
+/* ------------------------------------------- several GPUs, one host process */
+
+/* Replaces the reference's thread-pool tiler (WorkQueueCreate/WorkQueueStart,
+ * main.cpp:658-665, 851-856; wasm/wasm.cpp:651-678) with N GPUs driven from
+ * one host thread: the frame is dealt in interleaved BandRows-row bands,
+ * band b -> device b mod N, each device traces its bands on its
+ * own stream, and the band images are gathered to devices[0] over xGMI --
+ * RCCL grouped send/recv (ncclCommInitAll over the N devices) or, where RCCL
+ * cannot be used (a device listed twice, no librccl), peer copies
+ * (hipMemcpyPeerAsync) -- then scattered into the full frame.  Samples are
+ * never split across devices (the running-mean fold is order dependent,
+ * main.cpp:484-487), so the gathered frame is bit-identical to one device's. */
+typedef struct rt_multi rt_multi;
+
+#define RT_MULTI_AUTO 0u  /* RCCL when the devices are distinct and RCCL initialises, else peer copies */
+#define RT_MULTI_RCCL 1u  /* RCCL only (rt_multi_create fails if it cannot be used) */
+#define RT_MULTI_PEER 2u  /* peer copies only */
+#define RT_MULTI_MAX_DEVICES 16u
+
+int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t transport, rt_multi **out);
+int rt_multi_destroy(rt_multi *m);
+/* rt_set_rsqrt_table / rt_scene_upload on every device. */
+int rt_multi_set_rsqrt_table(rt_multi *m, const float table[2048]);
+int rt_multi_scene_upload(rt_multi *m, const rt_scene *scene);
+
+/* rt_trace over the N devices.  The running mean stays resident on the
+ * devices (each keeps its own bands'): desc->PreviousRayCount frames are
+ * already folded there by earlier calls of the same geometry, or
+ * RT_FLAG_ACCUM_ZERO (or PreviousRayCount 0) starts a new mean.
+ *   cam->CurrentImage.Data : DEVICE pointer on devices[0], the full
+ *                            Width x Height RGBA8 frame (written).
+ *   cam->PreviousImage.Data: NULL, or a DEVICE pointer on devices[0] that
+ *                            receives the full-frame v4 f32 running mean.
+ *   desc->BandRows         : band height, a multiple of 8 (0 = 8);
+ *                            desc->BandCount / BandIndex must be 0.
+ *   d_rays                 : DEVICE u64 on devices[0], incremented by the
+ *                            segments every device traced.
+ * Ordered after prior work on `stream` (a stream of devices[0]; NULL = the
+ * null stream); work enqueued on `stream` afterwards sees the gathered frame. */
+int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
+                   void *stream);
+int rt_multi_synchronize(rt_multi *m);
+
+typedef struct rt_multi_info {
+    uint32_t DeviceCount;
+    uint32_t Transport;      /* RT_MULTI_RCCL or RT_MULTI_PEER */
+    uint32_t BandRows;       /* of the last trace */
+    uint32_t MaxLocalRows;   /* rows of the largest device share */
+    uint64_t SegmentsFolded; /* dead-tile segments counted, not traced (last trace, all devices) */
+} rt_multi_info;
+int rt_multi_get_info(rt_multi *m, rt_multi_info *out);
+
+/* ----------------------------------- several GPUs, one process per GPU (RCCL) */
+
+/* The band gather for one-process-per-GPU launches (torch.distributed.run /
+ * mpirun): every rank traces its band residue with rt_trace (BandCount =
+ * nranks, BandIndex = rank) and rt_comm_gather_bands brings the compact band
+ * images to rank 0 over RCCL and scatters them into the full frame.  Rank 0
+ * makes the id (rt_comm_unique_id) and the launcher shares its
+ * RT_COMM_ID_BYTES bytes with every rank before rt_comm_create (which blocks
+ * until all ranks have joined).  RT_ENODEV when librccl cannot be loaded or
+ * RCCL refuses the communicator (e.g. two ranks on one GPU). */
+typedef struct rt_comm rt_comm;
+#define RT_COMM_ID_BYTES 128u
+int rt_comm_unique_id(void *id_out);
+int rt_comm_create(int hip_device, const void *id, uint32_t nranks, uint32_t rank, rt_comm **out);
+int rt_comm_destroy(rt_comm *c);
+/* d_local: this rank's compact band image (rt_band_local_rows(height,
+ * band_rows, nranks, rank) x width x elem_bytes, device); d_full: rank 0's
+ * full frame (width x height x elem_bytes, device; ignored elsewhere).
+ * Enqueued on `stream` (NULL = the null stream) on every rank. */
+int rt_comm_gather_bands(rt_comm *c, const void *d_local, void *d_full, uint32_t width, uint32_t height,
+                         uint32_t elem_bytes, uint32_t band_rows, void *stream);
+
 /* Scheduling counters accumulated over trace launches when the library is the
  * diagnostic build (`make -C simd-ray-tracer_amd variant NAME=stats
  * KFLAGS=-DRTK_STATS`, loaded via RT_TRACE_LIB) and the process runs with

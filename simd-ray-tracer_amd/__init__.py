@@ -93,6 +93,14 @@ class RtTraceInfo(ctypes.Structure):  # rt_trace_last_info
         "GroupsPerRuleSet")]
 
 
+class RtMultiInfo(ctypes.Structure):  # rt_multi_get_info
+    _fields_ = [(n, c_uint32) for n in ("DeviceCount", "Transport", "BandRows", "MaxLocalRows")] + [
+        ("SegmentsFolded", c_uint64)]
+
+
+RT_MULTI_AUTO, RT_MULTI_RCCL, RT_MULTI_PEER = 0, 1, 2
+RT_COMM_ID_BYTES = 128
+
 for _t, _n in ((RtV3, 16), (RtMaterial, 48), (RtScalarSphere, 80), (RtSphereGroup, 64), (RtArray, 16),
                (RtScene, 80), (RtImage, 24), (RtCameraInfo, 144), (RtRenderParams, 12)):
     assert ctypes.sizeof(_t) == _n, (_t.__name__, ctypes.sizeof(_t), _n)
@@ -117,6 +125,18 @@ SIGNATURES = {
     "rt_trace_last_info": (c_int, [c_void_p, POINTER(RtTraceInfo)]),
     "rt_encode_rgba8": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "rt_device_synchronize": (c_int, [c_void_p]),
+    "rt_multi_create": (c_int, [POINTER(c_int), c_uint32, c_uint32, POINTER(c_void_p)]),
+    "rt_multi_destroy": (c_int, [c_void_p]),
+    "rt_multi_set_rsqrt_table": (c_int, [c_void_p, c_void_p]),
+    "rt_multi_scene_upload": (c_int, [c_void_p, POINTER(RtScene)]),
+    "rt_multi_trace": (c_int, [c_void_p, POINTER(RtCameraInfo), POINTER(RtTraceDesc), c_void_p, c_void_p]),
+    "rt_multi_synchronize": (c_int, [c_void_p]),
+    "rt_multi_get_info": (c_int, [c_void_p, POINTER(RtMultiInfo)]),
+    "rt_comm_unique_id": (c_int, [c_void_p]),
+    "rt_comm_create": (c_int, [c_int, c_void_p, c_uint32, c_uint32, POINTER(c_void_p)]),
+    "rt_comm_destroy": (c_int, [c_void_p]),
+    "rt_comm_gather_bands": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32,
+                                     c_void_p]),
     "rt_debug_stats": (c_int, [c_void_p, c_void_p, c_int]),
     "rt_debug_wave_times": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
     "rt_debug_masks": (ctypes.c_int64, [c_void_p, c_void_p, c_uint64]),
@@ -347,6 +367,88 @@ class Device:
     def close(self) -> None:
         if self.handle:
             lib().rt_device_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Multi:
+    """Several GPUs from one process (rt_multi): interleaved row bands, one
+    device each, gathered to devices[0] over RCCL or peer copies."""
+
+    def __init__(self, devices, transport: int = RT_MULTI_AUTO, rsqrt_table: Optional[np.ndarray] = None):
+        devs = (c_int * len(devices))(*devices)
+        h = c_void_p()
+        _check(lib().rt_multi_create(devs, len(devices), transport, ctypes.byref(h)), "rt_multi_create")
+        self.handle = h
+        table = rsqrt_table_builtin() if rsqrt_table is None else np.ascontiguousarray(rsqrt_table, np.float32)
+        _check(lib().rt_multi_set_rsqrt_table(self.handle, table.ctypes.data), "rt_multi_set_rsqrt_table")
+
+    def upload_scene(self, scene: RtScene) -> None:
+        _check(lib().rt_multi_scene_upload(self.handle, ctypes.byref(scene)), "rt_multi_scene_upload")
+
+    def trace(self, cam: RtCameraInfo, *, width: int, height: int, cur_ptr: int, rays_ptr: int, prev_ptr: int = 0,
+              prev_count: int = 0, frames: int = 1, max_bounce: int = 5, simd: bool = True, band_rows: int = 8,
+              accum_zero: bool = False, srgb_pow: bool = False, stream: Optional[int] = None) -> None:
+        """Full-frame RGBA8 (and, with prev_ptr, the gathered running mean) on devices[0]."""
+        c = RtCameraInfo()
+        ctypes.pointer(c)[0] = cam
+        c.CurrentImage = RtImage(cur_ptr, width, height, RT_FORMAT_R8G8B8A8_U32)
+        c.PreviousImage = RtImage(prev_ptr or None, width, height, RT_FORMAT_R32B32G32A32_F32)
+        d = RtTraceDesc(width, height, prev_count, frames, max_bounce, 1 if simd else 0, RT_SEED_PIXEL, band_rows, 0, 0,
+                        (RT_FLAG_ACCUM_ZERO if accum_zero else 0) | (RT_FLAG_SRGB_POW if srgb_pow else 0))
+        _check(lib().rt_multi_trace(self.handle, ctypes.byref(c), ctypes.byref(d), c_void_p(rays_ptr),
+                                    c_void_p(stream or 0)), "rt_multi_trace")
+
+    def info(self) -> dict:
+        i = RtMultiInfo()
+        _check(lib().rt_multi_get_info(self.handle, ctypes.byref(i)), "rt_multi_get_info")
+        return {n: int(getattr(i, n)) for n, _ in RtMultiInfo._fields_}
+
+    def synchronize(self) -> None:
+        _check(lib().rt_multi_synchronize(self.handle), "rt_multi_synchronize")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().rt_multi_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(RT_COMM_ID_BYTES)
+    _check(lib().rt_comm_unique_id(buf), "rt_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """The RCCL band gather of a one-process-per-GPU launch (rt_comm)."""
+
+    def __init__(self, device: int, uid: bytes, nranks: int, rank: int):
+        assert len(uid) == RT_COMM_ID_BYTES
+        h = c_void_p()
+        buf = ctypes.create_string_buffer(uid, RT_COMM_ID_BYTES)
+        _check(lib().rt_comm_create(device, buf, nranks, rank, ctypes.byref(h)), "rt_comm_create")
+        self.handle = h
+
+    def gather_bands(self, local_ptr: int, full_ptr: int, width: int, height: int, elem_bytes: int, band_rows: int,
+                     stream: Optional[int] = None) -> None:
+        _check(lib().rt_comm_gather_bands(self.handle, c_void_p(local_ptr or None), c_void_p(full_ptr or None), width,
+                                          height, elem_bytes, band_rows, c_void_p(stream or 0)),
+               "rt_comm_gather_bands")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().rt_comm_destroy(self.handle)
             self.handle = None
 
     def __del__(self):  # pragma: no cover - best effort

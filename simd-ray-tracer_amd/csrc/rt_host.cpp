@@ -73,10 +73,24 @@ struct rt_device {
 
 static thread_local char g_err[512];
 
+static int vfail(int code, const char *fmt, va_list ap) {
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    return code;
+}
+
 static int fail(int code, const char *fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    vfail(code, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+// rt_kernel.h: the error text other translation units (rt_multi.cpp) report
+int rt_fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vfail(code, fmt, ap);
     va_end(ap);
     return code;
 }

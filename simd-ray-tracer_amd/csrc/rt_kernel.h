@@ -108,6 +108,10 @@ extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t
 // (dead pixels x frames) to the ray counter once.
 extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
                                 unsigned long long dead_rays, hipStream_t stream);
+// dst[0] += sum of slots[0, n) (the gathered per-device ray counters)
+extern "C" int rtk_launch_sum_u64(const uint64_t *slots, uint32_t n, uint64_t *dst, hipStream_t stream);
+// sets rt_last_error()'s text and returns `code` (rt_host.cpp)
+int rt_fail(int code, const char *fmt, ...);
 extern "C" int rtk_launch_encode(const void *accum, void *out, uint64_t n, uint32_t pow_mode, hipStream_t stream);
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream);

@@ -1531,6 +1531,18 @@ extern "C" int rtk_launch_encode(const void *accum, void *out, uint64_t n, uint3
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+__global__ void sum_u64_kernel(const uint64_t *slots, uint32_t n, uint64_t *dst) {
+    if (threadIdx.x != 0) return;
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < n; ++i) s += slots[i];
+    dst[0] += s;
+}
+
+extern "C" int rtk_launch_sum_u64(const uint64_t *slots, uint32_t n, uint64_t *dst, hipStream_t stream) {
+    hipLaunchKernelGGL(sum_u64_kernel, dim3(1), dim3(64), 0, stream, slots, n, dst);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *dst, uint32_t width, uint32_t height,
                                    uint32_t elem, uint32_t band_rows, uint32_t band_count, hipStream_t stream) {
     const dim3 block(256);

@@ -12,8 +12,48 @@ sys.path.insert(0, str(ROOT))
 import __graft_entry__ as graft  # noqa: E402
 
 
+MULTIRANK_OUT = ROOT / "gpurun_out" / "multirank_check.json"
+_multirank = {}
+
+
+def _selects_gpu(config) -> bool:
+    expr = (config.option.markexpr or "").replace(" ", "")
+    return "gpu" in expr and "notgpu" not in expr
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run on the GPU box")
+    # bench.py's multi-rank path runs as child processes (torchrun); they are
+    # started here, before this process touches the GPU, and
+    # tests/test_multirank_bench.py collects their result.
+    if _selects_gpu(config) and os.environ.get("RT_SKIP_MULTIRANK") != "1":
+        import subprocess
+        MULTIRANK_OUT.parent.mkdir(exist_ok=True)
+        if MULTIRANK_OUT.exists():
+            MULTIRANK_OUT.unlink()
+        log = open(MULTIRANK_OUT.with_suffix(".log"), "w")
+        _multirank["proc"] = subprocess.Popen([sys.executable, str(ROOT / "scripts" / "multirank_check.py"),
+                                               str(MULTIRANK_OUT)], cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
+
+
+def pytest_unconfigure(config):
+    p = _multirank.get("proc")
+    if p is not None and p.poll() is None:
+        try:
+            p.wait(timeout=300)
+        except Exception:
+            p.kill()
+
+
+@pytest.fixture(scope="session")
+def multirank_result():
+    """Result list of scripts/multirank_check.py (waits for it)."""
+    import json
+    p = _multirank.get("proc")
+    if p is None:
+        pytest.skip("multi-rank rehearsal not started (run with -m gpu)")
+    p.wait(timeout=280)
+    return json.loads(MULTIRANK_OUT.read_text())
 
 
 def _ensure_built():

@@ -35,16 +35,22 @@ CASES = [
     # configs[2] (C3) at full size: ~16x C2 on the CPU (minutes), so its CPU
     # re-render runs only with RT_SLOW_ORACLE=1 (tests/test_golden_regression.py)
     ("c3_full_3840x2160x1024", 1, 64, 3840, 2160, 1024, 8, True, "pixel"),
+    # bench.py's frames the primary-ray cull cannot empty: RTWeekend (sky term,
+    # 482 spheres) and C2's scene seen from inside the sphere cloud
+    ("rtw_full_1920x1080x64", 2, None, 1920, 1080, 64, 8, True, "pixel"),
+    ("c2in_full_1920x1080x256", 1, 64, 1920, 1080, 256, 8, True, "pixel"),
 ]
 SLOW = {"c3_full_3840x2160x1024"}
+# camera distance from the look-at point where a case does not use the scene's default
+DISTANCE = {"c2in_full_1920x1080x256": 1.0}
 
 
-def render_case(scene, n, W, H, frames, bounces, simd, seed):
+def render_case(scene, n, W, H, frames, bounces, simd, seed, distance=None):
     o = orc.scene_builtin(scene)
     if n is not None:
         o = o.prefix(n)
     mode = orc.SEED_PIXEL if seed == "pixel" else orc.SEED_STREAM
-    return orc.render(o, orc.camera(o, W, H), W, H, frames=frames, max_bounce=bounces, simd=simd,
+    return orc.render(o, orc.camera(o, W, H, distance=distance), W, H, frames=frames, max_bounce=bounces, simd=simd,
                       seed_mode=mode, threads=1 if seed == "stream" else orc.cpu_threads())
 
 
@@ -56,10 +62,11 @@ def main():
         if only and name not in only and name in keep:
             out[name] = keep[name]
             continue
-        prev, cur, rays = render_case(scene, n, W, H, frames, bounces, simd, seed)
+        prev, cur, rays = render_case(scene, n, W, H, frames, bounces, simd, seed, DISTANCE.get(name))
         mid = (H // 2) * W + W // 2
         out[name] = {"scene": scene, "spheres": n, "width": W, "height": H, "frames": frames, "bounces": bounces,
                      "simd": simd, "seed_mode": seed, "rays": rays,
+                     **({"distance": DISTANCE[name]} if name in DISTANCE else {}),
                      "fnv1a64_rgba8": f"{orc.fnv1a64(cur):016x}", "fnv1a64_v4": f"{orc.fnv1a64(prev):016x}",
                      "center_rgba8": f"{int(cur[mid]):08x}",
                      "center_v4_bits": [f"{int(v):08x}" for v in prev[mid].view(np.uint32)]}

@@ -24,7 +24,8 @@ def test_oracle_reproduces_golden(orc, name):
     if name in make_golden.SLOW and os.environ.get("RT_SLOW_ORACLE") != "1":
         pytest.skip("full-size C3 oracle render takes minutes: RT_SLOW_ORACLE=1")
     _, scene, n, W, H, frames, bounces, simd, seed = CASES[name]
-    prev, cur, rays = make_golden.render_case(scene, n, W, H, frames, bounces, simd, seed)
+    prev, cur, rays = make_golden.render_case(scene, n, W, H, frames, bounces, simd, seed,
+                                              make_golden.DISTANCE.get(name))
     g = GOLD[name]
     assert rays == g["rays"]
     assert f"{orc.fnv1a64(cur):016x}" == g["fnv1a64_rgba8"]
@@ -44,7 +45,7 @@ def test_gpu_matches_golden(rt, orc, torch_cuda, name):
     prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
     cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
     rays = torch.zeros(1, dtype=torch.int64, device="cuda")
-    dev.trace(rt.camera_setup(s, W, H), width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+    dev.trace(rt.camera_setup(s, W, H, distance=make_golden.DISTANCE.get(name)), width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
               rays_ptr=rays.data_ptr(), frames=frames, max_bounce=bounces, simd=simd)
     torch.cuda.synchronize()
     g = GOLD[name]

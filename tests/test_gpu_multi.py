@@ -1,0 +1,135 @@
+"""Several GPUs behind the C-ABI (rt_multi, rt_comm), on the one
+GPU of the test box: a device list may name cuda:0 more than once, which
+RCCL refuses, so those runs take the peer-copy transport; a one-device list
+runs the RCCL transport (grouped send/recv to itself).  Every gathered frame
+must be bit-identical to one device's rt_trace of the whole frame (and to the
+oracle): samples are never split across devices, so no bit may move."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def single(rt, torch, scene, cam, W, H, frames, B, simd=True, prev_count=0, prev=None):
+    dev = rt.Device(0)
+    try:
+        dev.upload_scene(scene)
+        if prev is None:
+            prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
+                  prev_count=prev_count, frames=frames, max_bounce=B, simd=simd, band_rows=8,
+                  stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        return prev, cur, int(rays.item())
+    finally:
+        dev.close()
+
+
+def multi_render(rt, torch, m, cam, W, H, frames, B, simd=True, prev_count=0, accum_zero=False, band_rows=8):
+    cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    prev = torch.full((W * H, 4), float("nan"), dtype=torch.float32, device="cuda")
+    rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    m.trace(cam, width=W, height=H, cur_ptr=cur.data_ptr(), prev_ptr=prev.data_ptr(), rays_ptr=rays.data_ptr(),
+            prev_count=prev_count, frames=frames, max_bounce=B, simd=simd, band_rows=band_rows,
+            accum_zero=accum_zero, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return prev, cur, int(rays.item())
+
+
+def same(a, b):
+    assert a[2] == b[2], (a[2], b[2])
+    assert torch_equal_bits(a[0], b[0]), "running mean differs"
+    assert torch_equal_bits(a[1], b[1]), "RGBA8 differs"
+
+
+def torch_equal_bits(x, y):
+    return np.array_equal(x.cpu().numpy().view(np.uint32), y.cpu().numpy().view(np.uint32))
+
+
+@pytest.mark.parametrize("devices,transport", [([0], "rccl"), ([0], "peer"), ([0, 0], "auto"), ([0, 0, 0], "auto"),
+                                               ([0] * 8, "auto")])
+def test_multi_equals_single_device(rt, orc, torch_cuda, devices, transport):
+    torch = torch_cuda
+    t = {"rccl": rt.RT_MULTI_RCCL, "peer": rt.RT_MULTI_PEER, "auto": rt.RT_MULTI_AUTO}[transport]
+    s = rt.scene_prefix(rt.scene_builtin(1), 64)
+    W, H, S, B = 200, 150, 4, 8  # 19 bands of 8 rows, the last one partial
+    cam = rt.camera_setup(s, W, H)
+    ref = single(rt, torch, s, cam, W, H, S, B)
+    m = rt.Multi(devices, t)
+    try:
+        info = m.info()
+        assert info["DeviceCount"] == len(devices)
+        assert info["Transport"] == (rt.RT_MULTI_RCCL if transport == "rccl" else rt.RT_MULTI_PEER)
+        m.upload_scene(s)
+        got = multi_render(rt, torch, m, cam, W, H, S, B, accum_zero=True)
+        same(got, ref)
+        o = orc.scene_builtin(1).prefix(64)
+        op, oc, orays = orc.render(o, orc.camera(o, W, H), W, H, frames=S, max_bounce=B)
+        assert orays == got[2] and np.array_equal(got[1].cpu().numpy().view(np.uint32), oc)
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_progressive_running_mean_stays_on_the_devices(rt, torch_cuda, devices):
+    """Frames 0-2 then 3-7 (PreviousRayCount 3, the running mean resident on
+    the devices) equal one 8-frame single-device launch; scalar rules too."""
+    torch = torch_cuda
+    s = rt.scene_builtin(0)
+    W, H, B = 96, 72, 5
+    cam = rt.camera_setup(s, W, H)
+    for simd in (True, False):
+        ref = single(rt, torch, s, cam, W, H, 8, B, simd=simd)
+        m = rt.Multi(devices)
+        try:
+            m.upload_scene(s)
+            a = multi_render(rt, torch, m, cam, W, H, 3, B, simd=simd)
+            b = multi_render(rt, torch, m, cam, W, H, 5, B, simd=simd, prev_count=3)
+            assert a[2] + b[2] == ref[2]
+            same((b[0], b[1], ref[2]), ref)
+        finally:
+            m.close()
+
+
+def test_multi_rejects_continuation_without_a_resident_mean(rt, torch_cuda):
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 16)
+    cam = rt.camera_setup(s, 64, 48)
+    m = rt.Multi([0, 0])
+    try:
+        m.upload_scene(s)
+        with pytest.raises(rt.RtError):
+            multi_render(rt, torch, m, cam, 64, 48, 2, 4, prev_count=2)
+        multi_render(rt, torch, m, cam, 64, 48, 2, 4)
+        with pytest.raises(rt.RtError):  # geometry changed: the resident mean is gone
+            multi_render(rt, torch, m, cam, 64, 40, 2, 4, prev_count=2)
+    finally:
+        m.close()
+
+
+def test_multi_rccl_refuses_a_device_listed_twice(rt, torch_cuda):
+    with pytest.raises(rt.RtError, match="RCCL"):
+        rt.Multi([0, 0], rt.RT_MULTI_RCCL)
+
+
+def test_comm_gather_single_rank(rt, orc, torch_cuda):
+    """rt_comm with one rank: the RCCL send/recv to itself plus the scatter
+    reproduce the compact band image as the full frame."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 64)
+    W, H, S, B = 120, 90, 3, 8
+    cam = rt.camera_setup(s, W, H)
+    ref = single(rt, torch, s, cam, W, H, S, B)
+    comm = rt.Comm(0, rt.comm_unique_id(), 1, 0)
+    try:
+        full = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        fullp = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        comm.gather_bands(ref[1].data_ptr(), full.data_ptr(), W, H, 4, 8, stream=st)
+        comm.gather_bands(ref[0].data_ptr(), fullp.data_ptr(), W, H, 16, 8, stream=st)
+        torch.cuda.synchronize()
+        assert torch.equal(full, ref[1]) and torch_equal_bits(fullp, ref[0])
+    finally:
+        comm.close()
