@@ -373,8 +373,12 @@ const char *rt_last_error(void);
 
 /* ----------------------------------------------- OnInit / OnRender driver */
 
-/* OnInit (main.cpp:645-679): window defaults, built-in scenes, device. */
+/* OnInit (main.cpp:645-679): window defaults, built-in scenes, device 0. */
 int rt_on_init(rt_init_params *params);
+/* OnInit on `count` devices: with more than one, rt_on_render drives them
+ * through rt_multi (bands dealt over the devices, the running mean resident
+ * on each, the frame gathered to hip_devices[0]). */
+int rt_on_init_devices(rt_init_params *params, const int *hip_devices, uint32_t count);
 
 /* Input state for the orbit camera (the reference polls IsDown(key) at
  * main.cpp:732-761).  Bits: */

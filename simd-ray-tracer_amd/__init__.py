@@ -146,6 +146,7 @@ SIGNATURES = {
                                   POINTER(c_uint32)]),
     "rt_last_error": (c_char_p, []),
     "rt_on_init": (c_int, [POINTER(RtInitParams)]),
+    "rt_on_init_devices": (c_int, [POINTER(RtInitParams), POINTER(c_int), c_uint32]),
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
     "rt_on_render_wait": (c_int, []),
     "rt_on_shutdown": (c_int, []),
@@ -473,9 +474,14 @@ def encode_rgba8(accum_ptr: int, rgba8_ptr: int, n_pixels: int, srgb_pow: bool =
 
 
 # ------------------------------------------------- OnInit / OnRender mirror
-def on_init() -> RtInitParams:
+def on_init(devices=None) -> RtInitParams:
+    """OnInit; `devices` (a list of HIP ordinals) drives several GPUs through rt_multi."""
     p = RtInitParams()
-    _check(lib().rt_on_init(ctypes.byref(p)), "rt_on_init")
+    if devices is None:
+        _check(lib().rt_on_init(ctypes.byref(p)), "rt_on_init")
+    else:
+        devs = (c_int * len(devices))(*devices)
+        _check(lib().rt_on_init_devices(ctypes.byref(p), devs, len(devices)), "rt_on_init_devices")
     return p
 
 

@@ -64,6 +64,8 @@ constexpr float kPi32 = 3.14159265358979323846f;
 struct App {
     bool ready = false;
     rt_device *dev = nullptr;
+    rt_multi *multi = nullptr;  // rt_on_init_devices with several devices
+    int ordinal = 0;            // hip_devices[0]: the frame, the counter and the stream live there
     uint32_t scene_index = 0xFFFFFFFFu;
     float distance = 0.0f, x_angle = 0.0f, y_height = 0.0f;
     uint32_t prev_count = 0;
@@ -97,6 +99,12 @@ int copy_current(const rt_image *image) {
 }  // namespace
 
 extern "C" int rt_on_init(rt_init_params *params) {
+    const int first = 0;
+    return rt_on_init_devices(params, &first, 1);
+}
+
+extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices, uint32_t count) {
+    if (!hip_devices || count == 0) return RT_EINVAL;
     if (params) {  // main.cpp:646-650
         static const char kTitle[] = "SIMD Ray Tracer";
         params->WindowTitle = kTitle;
@@ -108,12 +116,20 @@ extern "C" int rt_on_init(rt_init_params *params) {
     rt_scene s;
     int rc = rt_scene_builtin(0, &s);  // builds all three scenes (main.cpp:652-654)
     if (rc) return rc;
-    rc = rt_device_create(0, &g_app.dev);
-    if (rc) return rc;
     float table[2048];
     rt_rsqrt_table_builtin(table);
-    rc = rt_set_rsqrt_table(g_app.dev, table);
+    if (count > 1) {  // WorkQueueCreate's thread pool -> the devices (main.cpp:658-665)
+        rc = rt_multi_create(hip_devices, count, RT_MULTI_AUTO, &g_app.multi);
+        if (rc) return rc;
+        rc = rt_multi_set_rsqrt_table(g_app.multi, table);
+    } else {
+        rc = rt_device_create(hip_devices[0], &g_app.dev);
+        if (rc) return rc;
+        rc = rt_set_rsqrt_table(g_app.dev, table);
+    }
     if (rc) return rc;
+    g_app.ordinal = hip_devices[0];
+    if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
     if (hipMalloc(&g_app.d_rays, sizeof(uint64_t)) != hipSuccess ||
         hipEventCreate(&g_app.ev_start) != hipSuccess || hipEventCreate(&g_app.ev_done) != hipSuccess ||
         hipStreamCreateWithFlags(&g_app.stream, hipStreamNonBlocking) != hipSuccess)
@@ -127,12 +143,13 @@ extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint
                             uint64_t *out_total_rays_cast, double *out_time_elapsed_ms) {
     if (!g_app.ready || !image || image->Width == 0 || image->Height == 0) return RT_EINVAL;
     if (params.SceneIndex > 2) return RT_EINVAL;
+    if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
     bool moved = false;
     if (g_app.scene_index != params.SceneIndex) {  // main.cpp:718-727
         if (!frame_complete()) return 0;
         rt_scene sc;
         rt_scene_builtin(params.SceneIndex, &sc);
-        int rc = rt_scene_upload(g_app.dev, &sc);
+        int rc = g_app.multi ? rt_multi_scene_upload(g_app.multi, &sc) : rt_scene_upload(g_app.dev, &sc);
         if (rc) return rc;
         g_app.scene_index = params.SceneIndex;
         g_app.distance = sc.DefaultDistanceFromLookAt;
@@ -214,10 +231,17 @@ extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint
     desc.MaxBounce = 5;  // main.cpp:387
     desc.EnableSIMD = params.EnableSIMD ? 1u : 0u;
     desc.SeedMode = RT_SEED_PIXEL;
-    desc.BandRows = 32;
-    desc.BandCount = 1;
     if (hipEventRecord(g_app.ev_start, g_app.stream) != hipSuccess) return RT_EIO;
-    rc = rt_trace(g_app.dev, &g_app.cam, &desc, g_app.d_rays, g_app.stream);
+    if (g_app.multi) {  // the running mean stays on the devices, the frame is gathered into d_cur
+        desc.BandRows = 8;
+        if (g_app.prev_count == 0) desc.Flags |= RT_FLAG_ACCUM_ZERO;
+        g_app.cam.PreviousImage.Data = nullptr;
+        rc = rt_multi_trace(g_app.multi, &g_app.cam, &desc, g_app.d_rays, g_app.stream);
+    } else {
+        desc.BandRows = 32;
+        desc.BandCount = 1;
+        rc = rt_trace(g_app.dev, &g_app.cam, &desc, g_app.d_rays, g_app.stream);
+    }
     if (rc) return rc;
     if (hipEventRecord(g_app.ev_done, g_app.stream) != hipSuccess) return RT_EIO;
     g_app.in_flight = true;
@@ -236,6 +260,7 @@ extern "C" int rt_on_shutdown(void) {
     (void)hipEventDestroy(g_app.ev_done);
     (void)hipStreamDestroy(g_app.stream);
     rt_device_destroy(g_app.dev);
+    rt_multi_destroy(g_app.multi);
     g_app = App();
     return RT_OK;
 }

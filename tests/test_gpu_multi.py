@@ -133,3 +133,25 @@ def test_comm_gather_single_rank(rt, orc, torch_cuda):
         assert torch.equal(full, ref[1]) and torch_equal_bits(fullp, ref[0])
     finally:
         comm.close()
+
+
+def test_on_render_over_several_devices(rt, orc, torch_cuda):
+    """OnRender (one-frame lag, reset on scene switch) driving rt_multi: the
+    completed frames equal the oracle's progressive frames."""
+    rt.on_init(devices=[0, 0, 0])
+    try:
+        W, H = 64, 56
+        img = np.zeros((H, W), np.uint32)
+        o = orc.scene_builtin(2)
+        ocam = orc.camera(o, W, H)
+        done, _, _ = rt.on_render(img, 2)
+        assert not done
+        for k in range(3):
+            rt.on_render_wait()
+            done, rays, _ = rt.on_render(img, 2)
+            assert done
+            _, ocur, orays = orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5)
+            assert np.array_equal(img.reshape(-1), ocur), k
+        rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
