@@ -77,13 +77,8 @@ def rays(rng, centres, radii, n):
     return o, d
 
 
-@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 256), (0, None), (2, None)])
-@pytest.mark.parametrize("simd", [True, False])
-def test_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
-    scene = rt.scene_builtin(idx)
-    if n_spheres:
-        scene = rt.scene_prefix(scene, n_spheres)
-    r2, r2p, flags = rt.scene_prefilter(scene, simd)
+def slot_spheres(rt, scene, simd):
+    """Centres and radii per sphere slot 4*group+lane of one rule set."""
     sp, groups, _ = rt.scene_arrays(scene)
     if simd:
         cx_, cy_, cz_ = groups[:, 0:4].ravel(), groups[:, 4:8].ravel(), groups[:, 8:12].ravel()
@@ -92,11 +87,27 @@ def test_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
         pad = (-len(sp)) % 4
         cx_, cy_, cz_ = (np.concatenate([sp[:, k], np.zeros(pad, F)]) for k in range(3))
         radius = np.concatenate([sp[:, 4], np.zeros(pad, F)])
-    centres = np.stack([cx_, cy_, cz_], 1).astype(F)
+    return np.stack([cx_, cy_, cz_], 1).astype(F), radius
+
+
+@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 256), (0, None), (2, None)])
+@pytest.mark.parametrize("simd", [True, False])
+def test_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
+    scene = rt.scene_builtin(idx)
+    if n_spheres:
+        scene = rt.scene_prefix(scene, n_spheres)
+    check_prefilter(rt, scene, simd, 7 + idx)
+
+
+def check_prefilter(rt, scene, simd, seed, n_rays=4000, require_hits=True):
+    """No ray the bound is meant for has e >= r2p on a sphere its exact test
+    accepts; where the prefilter is on by default it must actually cull."""
+    r2, r2p, flags = rt.scene_prefilter(scene, simd)
+    centres, radius = slot_spheres(rt, scene, simd)
     assert np.array_equal(r2[: len(radius)][r2 >= 0], (radius * radius)[r2 >= 0])
     live = r2 > 0 if simd else r2 >= 0
-    rng = np.random.default_rng(7 + idx)
-    o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), 4000)
+    rng = np.random.default_rng(seed)
+    o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), n_rays)
     cx = centres[None, :, 0] - o[:, None, 0]
     cy = centres[None, :, 1] - o[:, None, 1]
     cz = centres[None, :, 2] - o[:, None, 2]
@@ -107,9 +118,11 @@ def test_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     hit &= live[None, :]
     skipped = ~(e < r2p)
     assert not np.any(hit & skipped), "prefilter skipped a sphere the exact test accepts"
-    assert hit.sum() > 0
+    if require_hits:
+        assert hit.sum() > 0
+    return bool(flags & 1), int((skipped & live[None, :]).sum())
 
-    if flags & 1:  # where it is enabled, the prefilter must actually cull
+    if flags & 1 and require_hits:  # where it is enabled, the prefilter must actually cull
         assert (~skipped).sum() < 1.5 * hit.sum() + 0.05 * hit.size
 
 
@@ -140,22 +153,24 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     scene = rt.scene_builtin(idx)
     if n_spheres:
         scene = rt.scene_prefix(scene, n_spheres)
+    if rt.scene_clusters(scene, simd)[1] == 0:
+        pytest.skip("scene uses the per-group prefilter loop")
+    check_clusters(rt, scene, simd, 11 + idx, require_culls=True)
+
+
+def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
+    """Decodes the cluster table; no skipped cluster (near-line or behind
+    rule) and no skipped member holds a sphere a lane can accept.  Returns
+    (rays x clusters skipped, of them by the behind rule)."""
     tab, ncp = rt.scene_clusters(scene, simd)
     r2, r2p, _ = rt.scene_prefilter(scene, simd)
     if ncp == 0:
-        pytest.skip("scene uses the per-group prefilter loop")
-    sp, groups, _ = rt.scene_arrays(scene)
-    if simd:
-        cx_, cy_, cz_ = groups[:, 0:4].ravel(), groups[:, 4:8].ravel(), groups[:, 8:12].ravel()
-        radius = groups[:, 12:16].ravel()
-    else:
-        pad = (-len(sp)) % 4
-        cx_, cy_, cz_ = (np.concatenate([sp[:, k], np.zeros(pad, F)]) for k in range(3))
-        radius = np.concatenate([sp[:, 4], np.zeros(pad, F)])
-    centres = np.stack([cx_, cy_, cz_], 1).astype(F)
+        return 0, 0
+    centres, radius = slot_spheres(rt, scene, simd)
     live = np.isfinite(r2p)
     # decode the table: clusters -> member spheres (by centre and r2p) and pair indices
     members = []
+    used = set()
     beta_of = {}  # per-sphere behind threshold (member rows)
     for c in range(ncp):
         q = tab[c]
@@ -182,26 +197,30 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
                     assert len(s) >= 1
                     s = [k for k in s if pair[w] == int(k) >> 1]
                     assert len(s) >= 1, "member pair index is not its sphere's pair in group order"
+                    s = [k for k in s if k not in used] or s  # two spheres of one pair with equal rows
+                    used.add(s[0])
                     ms.append(s[0])
                     beta_of[s[0]] = np.float32(e[3][w])
             members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
                             np.float32(q[1][2 + h]), ms, np.float32(q[3][h])))
     covered = sorted(s for m in members for s in m[4])
     assert covered == sorted(np.flatnonzero(live)), "every hittable sphere is in exactly one cluster"
-    rng = np.random.default_rng(11 + idx)
-    o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), 4000)
+    rng = np.random.default_rng(seed)
+    o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), n_rays)
     dx, dy, dz = d[:, None, 0], d[:, None, 1], d[:, None, 2]
     cx = centres[None, :, 0] - o[:, None, 0]
     cy = centres[None, :, 1] - o[:, None, 1]
     cz = centres[None, :, 2] - o[:, None, 2]
     accept = could_accept(cx, cy, cz, dx, dy, dz, r2[None, :], simd) & live[None, :]
-    assert accept.sum() > 0
+    if require_culls:
+        assert accept.sum() > 0
     # sphere level: near-line estimate or wholly behind the origin (member rows)
     e_s, t_s = prefilter(cx, cy, cz, dx, dy, dz, with_t=True)
     beta = np.array([beta_of.get(k, -np.inf) for k in range(len(r2))], F)
     skip_s = ~(e_s < r2p[None, :]) | (t_s < beta[None, :])
     assert not np.any(accept & skip_s), "the member test skipped a sphere a lane can accept"
-    assert np.any((t_s < beta[None, :]) & (e_s < r2p[None, :]) & live[None, :]), "the behind rule culls nothing"
+    if require_culls:
+        assert np.any((t_s < beta[None, :]) & (e_s < r2p[None, :]) & live[None, :]), "the behind rule culls nothing"
     skipped_any = behind_any = 0
     for qx, qy, qz, t, ms, bc in members:
         if np.isneginf(t):
@@ -213,4 +232,6 @@ def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
         skipped_any += int(skip.sum())
         behind_any += int((behind & (ex[:, 0] < t)).sum())
         assert not np.any(accept[skip][:, ms]), "a skipped cluster holds a sphere a lane can accept"
-    assert skipped_any > 0 and behind_any > 0  # both cluster rules cull
+    if require_culls:
+        assert skipped_any > 0 and behind_any > 0  # both cluster rules cull
+    return skipped_any, behind_any
