@@ -166,9 +166,12 @@ int rt_rsqrt_table_capture_host(float table_out[2048]);
 
 /* Uploads Scenes[SceneIndex] (read by RenderTile at main.cpp:370) into
  * HBM: SIMDSpheres/Materials for the SIMD rules, ScalarSpheres for the
- * scalar rules.  The scene is copied; the caller keeps ownership.
+ * scalar rules.  The scene is copied; the caller keeps ownership.  Scenes
+ * up to 1,060 spheres (265 groups) are also staged in each block's LDS; larger
+ * ones, up to RT_MAX_SPHERES, are read from HBM through the caches.
  * RT_EINVAL for a scene with no spheres (every built-in scene has some) or
- * more than the LDS-staged limit (rt_kernel.h kMaxLdsGroups groups). */
+ * more than RT_MAX_SPHERES. */
+#define RT_MAX_SPHERES 16384u
 int rt_scene_upload(rt_device *dev, const rt_scene *scene);
 
 /* --------------------------------------------------------------- tracing */

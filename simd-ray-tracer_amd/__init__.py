@@ -28,6 +28,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / os.environ.get("RT_TRACE_LIB", "librt_trace.so")
 
 RT_SEED_PIXEL = 1
+RT_MAX_SPHERES = 16384
 RT_FLAG_ACCUM_ZERO = 1
 RT_FLAG_SRGB_POW = 2
 RT_FORMAT_R32B32G32A32_F32 = 1

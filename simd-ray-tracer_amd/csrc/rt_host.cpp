@@ -43,6 +43,7 @@ struct rt_device {
     // image are in)
     int clusters_env = 1;
     int interleave_env = 0;  // RT_INTERLEAVE=1: wave tiles interleaved over the block tile (P >= 2)
+    int scene_global_env = 0;  // RT_SCENE_GLOBAL=1: keep the scene in HBM even when the LDS image could hold it
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
@@ -138,6 +139,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (ol) d->order_launches = (uint32_t)atoi(ol);
     const char *il = getenv("RT_INTERLEAVE");
     if (il && (il[0] == '0' || il[0] == '1')) d->interleave_env = il[0] - '0';
+    const char *sg = getenv("RT_SCENE_GLOBAL");
+    if (sg && sg[0] == '1') d->scene_global_env = 1;
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -534,8 +537,8 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
     if (ng == 0 || !scene->SIMDSpheres.Data || !scene->Materials.Data || ns == 0 || !scene->ScalarSpheres.Data)
         return fail(RT_EINVAL, "scene: empty scene");
     const uint32_t ngs = (ns + 3u) / 4u;
-    if (ng > kMaxLdsGroups || ngs > kMaxLdsGroups)
-        return fail(RT_EINVAL, "scene: %u spheres exceed the LDS-staged limit of %u", ns, 4u * kMaxLdsGroups);
+    if (ng > kMaxGroups || ngs > kMaxGroups)
+        return fail(RT_EINVAL, "scene: %u spheres exceed the limit of %u", ns, 4u * kMaxGroups);
     const uint32_t n = rs == 0 ? ng : ngs;
     p.n_groups = n;
     p.groups.assign((size_t)n * 4 * kGroupF4, 0.0f);
@@ -746,6 +749,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.interleave = d->interleave_env && lpp >= 2 ? 1u : 0u;
     a.lut_in_lds = rtk_lut_in_lds(a.n_groups) ? 1u : 0u;
     a.fold_in_lds = rtk_fold_in_lds(a.n_groups) ? 1u : 0u;
+    a.scene_in_lds = a.n_groups <= kMaxLdsGroups && !d->scene_global_env ? 1u : 0u;
+    const int src = a.scene_in_lds ? d->src : kSrcSmem;  // a scene in HBM is read through the scalar cache
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     const bool cull = d->cull != 0;
@@ -839,7 +844,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     d->last.OrderedLaunches = d->n_sorts;
     d->last.ClusteredWalk = a.clusters ? 1u : 0u;
     d->last.GroupsPerRuleSet = a.n_groups;
-    if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, d->src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
+    if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
         return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     if (empty_capable && d->n_live < n_tiles &&
         rtk_launch_empty(&a, lpp, d->d_tile_live, (unsigned long long)(d->dead_pixels * desc->Frames), s) != 0)

@@ -62,6 +62,7 @@ struct TraceArgs {
     uint32_t interleave;         // wave tiles interleave over the block tile (P >= 2 only)
     uint32_t lut_in_lds;         // rsqrt table in the LDS image (else read from HBM: rtk_lut_in_lds)
     uint32_t fold_in_lds;        // running-mean weight table in the LDS image (else computed: rtk_fold_in_lds)
+    uint32_t scene_in_lds;       // groups + materials copied into the LDS image (else read from HBM: GS kernels)
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
@@ -78,11 +79,18 @@ constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 // weights are then two divisions per sample): C5 fits 7 blocks per CU.
 static inline bool rtk_lut_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
 static inline bool rtk_fold_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
-static inline size_t rtk_lds_bytes(uint32_t n_groups) {
-    return (rtk_lut_in_lds(n_groups) ? 8192u : 0u) + (rtk_fold_in_lds(n_groups) ? 2048u : 0u) +
-           (size_t)n_groups * (16u * kGroupF4) + (size_t)n_groups * 128u;
+static inline size_t rtk_scene_lds_bytes(uint32_t n_groups) { return (size_t)n_groups * (16u * kGroupF4 + 128u); }
+static inline size_t rtk_lds_bytes(const TraceArgs *a) {
+    return (a->lut_in_lds ? 8192u : 0u) + (a->fold_in_lds ? 2048u : 0u) +
+           (a->scene_in_lds ? rtk_scene_lds_bytes(a->n_groups) : 0u);
 }
+// The largest scene the LDS image holds (64 KB of dynamic LDS per block with
+// the two tables): 265 groups = 1,060 spheres.  Larger scenes stay in HBM
+// (scene_in_lds = 0): the sphere loop reads groups through the scalar cache as
+// always, and the per-lane gathers go through L1/L2.  Up to kMaxGroups groups
+// (the primary cull masks are kMaxGroups / 64 words per wave tile).
 static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4 + 128u);  // 265 groups
+static const uint32_t kMaxGroups = 4096u;                                                    // 16,384 spheres
 
 extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
                                 hipStream_t stream);

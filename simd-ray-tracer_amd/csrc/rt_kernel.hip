@@ -466,10 +466,12 @@ __device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz
 // The exact recheck of one group's flagged sphere pairs (f01, f23): only such
 // a pair reruns the exact packed test (same ops as test_group) and the exact
 // candidate logic decides, so results are identical.
-template <bool SIMD>
+// GS (scenes beyond the LDS image, rt_kernel.h kMaxLdsGroups): the group's r^2
+// row (wave-uniform g) comes through the scalar cache instead of LDS.
+template <bool SIMD, bool GS>
 __device__ __forceinline__ void recheck_pairs(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
                                               const RayPk &p, Hit &h, bool f01, bool f23) {
-    const float4 r2 = lds_groups[kGroupF4 * g + kRowR2];
+    const float4 r2 = GS ? f4(((cv4f_t *)a.groups)[kGroupF4 * g + kRowR2]) : lds_groups[kGroupF4 * g + kRowR2];
     if (f01) {
         f2 T01;
         const f2 d01 = pair_dist(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
@@ -506,7 +508,7 @@ struct PfStats {
     uint32_t groups, groups_noown, pairs, pairs_noown, lane_pairs;
 };
 
-template <bool SIMD>
+template <bool SIMD, bool GS>
 __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
                                               const RayPk &p, Hit &h, uint32_t own = ~0u, PfStats *ps = nullptr) {
     bool f01, f23;
@@ -525,7 +527,7 @@ __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *
         ps->pairs_noown += (__ballot(n01) != 0) + (__ballot(n23) != 0);
         ps->lane_pairs += __builtin_popcountll(__ballot(f01)) + __builtin_popcountll(__ballot(f23));
     }
-    if (f01 | f23) recheck_pairs<SIMD>(a, lds_groups, G, g, p, h, f01, f23);
+    if (f01 | f23) recheck_pairs<SIMD, GS>(a, lds_groups, G, g, p, h, f01, f23);
 }
 
 template <bool SIMD>
@@ -542,7 +544,7 @@ __device__ __forceinline__ Group load_group_pf_at(cv4f_t *cg) {
 
 // The full sphere loop over all groups from SGPRs.  PF: secondary rays
 // through the prefilter; else the exact test.
-template <bool SIMD, bool PF>
+template <bool SIMD, bool PF, bool GS>
 __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray, Hit &h,
                                                 uint32_t *hit_groups, uint32_t own = ~0u, PfStats *ps = nullptr) {
     cv4f_t *gp = (cv4f_t *)a.groups;
@@ -552,7 +554,7 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
     // measured 2 % slower)
     for (uint32_t g = 0; g < a.n_groups; ++g, gp += kGroupF4) {
         const Group G = PF ? load_group_pf_at(gp) : load_group_at(gp);
-        if (PF) test_group_pf<SIMD>(a, lds_groups, G, g, ray, h, own, ps);
+        if (PF) test_group_pf<SIMD, GS>(a, lds_groups, G, g, ray, h, own, ps);
         else test_group<SIMD>(a, G, g, ray, h, hit_groups);
     }
 }
@@ -600,7 +602,7 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
 
 // ps (RTK_STATS): groups += member-pair entries tested, pairs += sphere pairs
 // rechecked exactly, lane_pairs += clusters entered (per wave).
-template <bool SIMD, int W>
+template <bool SIMD, int W, bool GS>
 __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray,
                                                  Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
@@ -627,7 +629,7 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
             const bool f01 = (m >> q) & 1u, f23 = (m >> (q + 1u)) & 1u;
             m &= ~(3ull << q);
             if (ps) ps->pairs += (f01 ? 1u : 0u) + (f23 ? 1u : 0u);
-            recheck_pairs<SIMD>(a, lds_groups, load_group_pf_at(gp + kGroupF4 * g), g, ray, h, f01, f23);
+            recheck_pairs<SIMD, GS>(a, lds_groups, load_group_pf_at(gp + kGroupF4 * g), g, ray, h, f01, f23);
         }
     }
 }
@@ -740,7 +742,12 @@ constexpr bool kStats = false;
 #endif
 
 constexpr int kWavesPerBlock = 4;
-constexpr int kMaxMaskWords = (kMaxLdsGroups + 63) / 64;
+// primary group mask words per wave tile: the LDS-image kernels keep this
+// small (it is static LDS, and C2's blocks fill the CU's 160 KB 7 times)
+template <bool GS>
+struct MaskWords {
+    static constexpr int N = GS ? (int)((kMaxGroups + 63u) / 64u) : (int)((kMaxLdsGroups + 63u) / 64u);
+};
 constexpr uint32_t kFoldTable = 256;
 // Per-pixel out-of-order sample slots (LDS ring): at least P (every sample
 // lane holds one sample in flight) plus slack.
@@ -769,15 +776,18 @@ struct Shape {
     static_assert(TW * TH * P == 64, "a wave is 64 lanes");
 };
 
-template <bool SIMD, int SRC, bool CULL, int P>
+// GS: the scene (groups + materials) stays in HBM and per-lane gathers read it
+// through the caches (scenes beyond the LDS image, or RT_SCENE_GLOBAL=1).
+template <bool SIMD, int SRC, bool CULL, int P, bool GS>
 __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) void trace_kernel(TraceArgs a) {
+    static_assert(!GS || SRC == kSrcSmem, "a scene in HBM is read through the scalar cache");
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
     constexpr uint32_t kRing = Ring<P>::N;
     extern __shared__ float4 smem[];
     const uint64_t st_entry = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
-    __shared__ uint64_t s_mask[kWavesPerBlock][kMaxMaskWords];
+    __shared__ uint64_t s_mask[kWavesPerBlock][MaskWords<GS>::N];
     // ring slot s of pixel pl at s * kRingStride + pl: the sample lanes of a
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
@@ -789,11 +799,16 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     const uint32_t fold_n = a.fold_in_lds ? kFoldTable : 0u;
     float4 *lds_groups = smem + lut_f4 + fold_n / 2;
     float4 *lds_mats = lds_groups + kGroupF4 * a.n_groups;
+    // per-lane gathers of the winner's centre and material: LDS image or HBM (GS)
+    const float *sph_src = GS ? reinterpret_cast<const float *>(a.groups) : reinterpret_cast<const float *>(lds_groups);
+    const float4 *mat_src = GS ? a.materials : lds_mats;
     {
         const float4 *glut = reinterpret_cast<const float4 *>(a.rsqrt_lut);
         for (uint32_t i = threadIdx.x; i < lut_f4; i += blockDim.x) smem[i] = glut[i];
-        for (uint32_t i = threadIdx.x; i < kGroupF4 * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
-        for (uint32_t i = threadIdx.x; i < 8u * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
+        if (!GS) {
+            for (uint32_t i = threadIdx.x; i < kGroupF4 * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
+            for (uint32_t i = threadIdx.x; i < 8u * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
+        }
         // running-mean weights of frame k (main.cpp:484-487): 1/(p+1), p/(p+1)
         for (uint32_t i = threadIdx.x; i < fold_n; i += blockDim.x) {
             const uint32_t pc = a.prev_count + i;
@@ -958,14 +973,15 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         if (SRC == kSrcSmem && pf && a.n_cpairs) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             PfStats *ps = kStats && a.stats ? &st_pf : nullptr;
-                            if (a.cl_words == 1u) clustered_groups<SIMD, 1>(a, lds_groups, ray, h, ps);
-                            else clustered_groups<SIMD, 2>(a, lds_groups, ray, h, ps);
+                            if (a.cl_words == 1u) clustered_groups<SIMD, 1, GS>(a, lds_groups, ray, h, ps);
+                            else clustered_groups<SIMD, 2, GS>(a, lds_groups, ray, h, ps);
                         } else if (SRC == kSrcSmem && pf) {
                             if (kStats && a.stats) st_pf_rounds += 1;
-                            all_groups_smem<SIMD, true>(a, lds_groups, ray, h, nullptr, p.own,
+                            all_groups_smem<SIMD, true, GS>(a, lds_groups, ray, h, nullptr, p.own,
                                                         kStats && a.stats ? &st_pf : nullptr);
                         } else if (SRC == kSrcSmem) {
-                            all_groups_smem<SIMD, false>(a, lds_groups, ray, h, kStats && a.stats ? &st_sec_hit : nullptr);
+                            all_groups_smem<SIMD, false, GS>(a, lds_groups, ray, h,
+                                                             kStats && a.stats ? &st_sec_hit : nullptr);
                         } else {
                             // software-pipelined: group g+1's load is in flight while
                             // g is tested (the array carries padding groups)
@@ -1006,7 +1022,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     } else {
                         // Re-derive the winner's HitNormal / NextRayOrigin exactly as
                         // they were formed at acceptance (main.cpp:423-429).
-                        const float *gsph = reinterpret_cast<const float *>(lds_groups) + 4u * kGroupF4 * (sidx >> 2) + (sidx & 3u);
+                        const float *gsph = sph_src + 4u * kGroupF4 * (sidx >> 2) + (sidx & 3u);
                         const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
                         const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
                         const float ipx = p.rx.y * tmin, ipy = p.ry.y * tmin, ipz = p.rz.y * tmin;
@@ -1014,8 +1030,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         p.rx.x = p.rx.x + ipx;
                         p.ry.x = p.ry.x + ipy;
                         p.rz.x = p.rz.x + ipz;
-                        const float4 cs = lds_mats[2u * sidx + 0u];
-                        const float4 ei = lds_mats[2u * sidx + 1u];
+                        const float4 cs = mat_src[2u * sidx + 0u];
+                        const float4 ei = mat_src[2u * sidx + 1u];
                         shade(lut, cs, ei, hx, hy, hz, inside, p);
                         if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
                         p.bounce += 1;
@@ -1435,18 +1451,28 @@ extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lane
 template <int P>
 static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks, hipStream_t stream) {
     const dim3 block(256), grid(n_blocks);
-    const size_t lds = rtk_lds_bytes(a->n_groups);
-#define RTK_LAUNCH(S, R, C) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P>), grid, block, lds, stream, *a)
+    const size_t lds = rtk_lds_bytes(a);
+#define RTK_LAUNCH(S, R, C, G) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P, G>), grid, block, lds, stream, *a)
+    if (!a->scene_in_lds) {  // the scene in HBM (the host picks the SMEM source for it)
+        const int key = (simd ? 2 : 0) | (cull ? 1 : 0);
+        switch (key) {
+            case 0: RTK_LAUNCH(false, kSrcSmem, false, true); break;
+            case 1: RTK_LAUNCH(false, kSrcSmem, true, true); break;
+            case 2: RTK_LAUNCH(true, kSrcSmem, false, true); break;
+            default: RTK_LAUNCH(true, kSrcSmem, true, true); break;
+        }
+        return;
+    }
     const int key = (simd ? 4 : 0) | (src == kSrcLds ? 2 : 0) | (cull ? 1 : 0);
     switch (key) {
-        case 0: RTK_LAUNCH(false, kSrcSmem, false); break;
-        case 1: RTK_LAUNCH(false, kSrcSmem, true); break;
-        case 2: RTK_LAUNCH(false, kSrcLds, false); break;
-        case 3: RTK_LAUNCH(false, kSrcLds, true); break;
-        case 4: RTK_LAUNCH(true, kSrcSmem, false); break;
-        case 5: RTK_LAUNCH(true, kSrcSmem, true); break;
-        case 6: RTK_LAUNCH(true, kSrcLds, false); break;
-        default: RTK_LAUNCH(true, kSrcLds, true); break;
+        case 0: RTK_LAUNCH(false, kSrcSmem, false, false); break;
+        case 1: RTK_LAUNCH(false, kSrcSmem, true, false); break;
+        case 2: RTK_LAUNCH(false, kSrcLds, false, false); break;
+        case 3: RTK_LAUNCH(false, kSrcLds, true, false); break;
+        case 4: RTK_LAUNCH(true, kSrcSmem, false, false); break;
+        case 5: RTK_LAUNCH(true, kSrcSmem, true, false); break;
+        case 6: RTK_LAUNCH(true, kSrcLds, false, false); break;
+        default: RTK_LAUNCH(true, kSrcLds, true, false); break;
     }
 #undef RTK_LAUNCH
 }

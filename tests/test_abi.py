@@ -145,14 +145,15 @@ def test_trace_rejects_bad_arguments(rt):
 
 def test_scene_size_limits(rt):
     """rt_scene_upload's packer (shared with rt_scene_prefilter, no GPU needed)
-    rejects an empty scene and one past the LDS-staged limit (265 groups)."""
+    rejects an empty scene and one past RT_MAX_SPHERES; scenes past the LDS
+    image's 1,060 spheres are accepted (they stay in HBM)."""
     empty = rt.scene_from_spheres(np.zeros((0, 20), np.float32), use_sky=True)
     with pytest.raises(rt.RtError, match="empty scene"):
         rt.scene_prefilter(empty, True)
-    sp = np.zeros((4 * 265 + 1, 20), np.float32)
+    sp = np.zeros((rt.RT_MAX_SPHERES + 1, 20), np.float32)
     sp[:, 0] = np.arange(len(sp), dtype=np.float32)
     sp[:, 4] = 0.25
-    with pytest.raises(rt.RtError, match="LDS-staged limit"):
+    with pytest.raises(rt.RtError, match="exceed the limit"):
         rt.scene_prefilter(rt.scene_from_spheres(sp[:]), True)
-    r2, _, _ = rt.scene_prefilter(rt.scene_from_spheres(sp[:-1]), True)  # exactly at the limit
-    assert len(r2) == 4 * 265
+    r2, _, _ = rt.scene_prefilter(rt.scene_from_spheres(sp[:4 * 265 + 1]), True)  # one past the LDS image
+    assert len(r2) == 4 * 266

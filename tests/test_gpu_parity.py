@@ -230,7 +230,8 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
 VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"},
                 {"RT_INTERLEAVE": "1"}, {"RT_CULL": "0"}, {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"},
                 {"RT_LANES_PER_PIXEL": "32"}, {"RT_SEC_THRESHOLD": "1"}, {"RT_SPHERE_SRC": "lds"},
-                {"RT_SPHERE_SRC": "lds", "RT_CULL": "0"}, {"RT_SPHERE_SRC": "lds", "RT_CLUSTERS": "0"}]
+                {"RT_SPHERE_SRC": "lds", "RT_CULL": "0"}, {"RT_SPHERE_SRC": "lds", "RT_CLUSTERS": "0"},
+                {"RT_SCENE_GLOBAL": "1"}, {"RT_SCENE_GLOBAL": "1", "RT_CULL": "0"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
@@ -478,3 +479,39 @@ def test_upload_waits_for_traces_in_flight(rt, orc, torch_cuda):
     for (p, c, n), o in zip(out, (oa, ob)):
         r = orc.render(o, orc.camera(o, W, H), W, H, frames=S, max_bounce=B)
         assert_same(p, c, n, *r)
+
+
+@pytest.mark.parametrize("n_spheres", [1061, 2000, 4099])
+def test_scene_beyond_the_lds_image(rt, orc, torch_cuda, gdev, n_spheres):
+    """Scenes above 1,060 spheres (265 groups) stay in HBM: the sphere loop
+    reads groups through the scalar cache and the winner / material / r^2
+    gathers go through the caches.  RTWeekend's 482 spheres plus small spheres
+    scattered over its ground, both rule sets, bit-exact against the oracle."""
+    base = rt.scene_builtin(2)
+    sp0, _, _ = rt.scene_arrays(base)
+    rng = np.random.default_rng(n_spheres)
+    extra = sp0[rng.integers(1, len(sp0), n_spheres - len(sp0))].copy()
+    extra[:, 0] = rng.uniform(-1.5, 1.5, len(extra))
+    extra[:, 2] = rng.uniform(-1.5, 1.5, len(extra))
+    extra[:, 4] = rng.uniform(0.004, 0.015, len(extra))
+    extra[:, 1] = extra[:, 4]
+    sp = np.concatenate([sp0, extra]).astype(np.float32)
+    la = (base.LookAt.x, base.LookAt.y, base.LookAt.z)
+    kw = dict(distance=base.DefaultDistanceFromLookAt, x_angle=base.DefaultXAngle, y_height=base.DefaultYHeight)
+    s = rt.scene_from_spheres(sp, look_at=la, use_sky=True, **kw)
+    _, groups, mats = rt.scene_arrays(s)
+    assert len(groups) > 265
+    o = orc.Scene(sp, groups, mats, look_at=la, use_sky=True, **kw)
+    W, H = 40, 24
+    cam = rt.camera_setup(s, W, H)
+    for simd in (True, False):
+        g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5, simd=simd)
+        r = orc.render(o, orc.camera(o, W, H), W, H, frames=2, max_bounce=5, simd=simd)
+        assert_same(*g, *r)
+
+
+def test_scene_above_the_limit_is_refused(rt, torch_cuda, gdev):
+    sp = np.zeros((int(rt.RT_MAX_SPHERES) + 1, 20), np.float32)
+    sp[:, 4] = 0.1
+    with pytest.raises(rt.RtError, match="exceed"):
+        gdev.upload_scene(rt.scene_from_spheres(sp))
