@@ -359,8 +359,11 @@ int64_t rt_debug_masks(rt_device *dev, uint64_t *out, uint64_t max_words);
  * and the secondary-ray prefilter threshold r2p (any ray whose
  * origin lies on a scene sphere and |D|^2 is within 2^-16 of 1 that passes
  * the exact test d < r^2 (d <= r^2 for the scalar rules) has prefilter
- * estimate e < r2p).  *out_flags: bit 0 = prefilter enabled by default for
- * this scene, bit 1 = candidate sqrt in the short sequence's range.
+ * estimate e < r2p).  *out_flags: bit 0 = the scene-wide threshold pays
+ * for this scene, bit 1 = candidate sqrt in the short sequence's range, bit 2
+ * = per-lane thresholds instead (where bit 0 is clear): r2p then holds r^2
+ * (-inf: never hit) and a lane skips a sphere when e >= RN(cc 2^-15 + r2p),
+ * cc its computed |C|^2.
  * Arrays may be NULL to query the count. */
 int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p, uint32_t capacity,
                        uint32_t *out_count, uint32_t *out_flags);

@@ -31,6 +31,8 @@ struct rt_device {
     uint32_t sec_threshold = 16;
     int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
+    uint32_t pf_relative[2] = {0, 0};  // per rule set: row 3 holds r^2, per-lane thresholds (rt_kernel.hip kPfRel)
+    int pf_rel_env = -1;  // RT_PF_REL: -1 auto (relative where the scene-wide bound does not pay), 0 never, 1 always
     uint32_t fast_sqrt[2] = {0, 0};  // per rule set: candidate sqrt in sqrt_rn's verified range
     float4 *d_clusters[2] = {nullptr, nullptr};  // clustered prefilter tables (cluster_table)
     size_t cap_clusters[2] = {0, 0};             // float4 capacity
@@ -131,6 +133,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (thr) d->sec_threshold = (uint32_t)atoi(thr);
     const char *pf = getenv("RT_PREFILTER");  // secondary-ray prefilter: 0 off, 1 on, unset = per-scene auto
     if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
+    const char *pr = getenv("RT_PF_REL");
+    if (pr && (pr[0] == '0' || pr[0] == '1')) d->pf_rel_env = pr[0] - '0';
     const char *to = getenv("RT_TILE_ORDER");
     if (to && to[0] == '0') d->tile_sched = 0;
     const char *clu = getenv("RT_CLUSTERS");
@@ -526,12 +530,13 @@ struct PackedSet {
     std::vector<float> groups, mats;
     uint32_t n_groups = 0;
     bool prefilter_pays = false;
+    bool relative = false;  // row 3 rewritten to r^2 / -inf for the per-lane threshold
     uint32_t fast_sqrt = 0;
     std::vector<float> clusters;  // cluster_table
     uint32_t n_cpairs = 0, cl_words = 0;
 };
 
-static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
+static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env = -1) {
     const uint32_t ng = scene->SIMDSpheres.Count;
     const uint32_t ns = scene->ScalarSpheres.Count;
     if (ng == 0 || !scene->SIMDSpheres.Data || !scene->Materials.Data || ns == 0 || !scene->ScalarSpheres.Data)
@@ -571,7 +576,20 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p) {
     }
     p.prefilter_pays = prefilter_rows(gv, n, rs == 0);
     p.fast_sqrt = sqrt_range_ok(gv, n, rs == 0);
-    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words);
+    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words);  // (member rows keep the scene-wide r2p)
+    // Where the scene-wide bound M_j makes r2p useless (a huge sphere: RTWeekend's
+    // ground), the per-group loop forms its threshold per lane from the lane's own
+    // |C|^2 instead (rt_kernel.hip kPfRel): row 3 then holds r^2 (-inf: never hit).
+    p.relative = pf_rel_env == 1 || (pf_rel_env < 0 && !p.prefilter_pays);
+    if (p.relative) {  // (the cluster table's scene-wide thresholds would not pay either)
+        p.n_cpairs = 0;
+        p.clusters.clear();
+    }
+    if (p.relative)
+        for (uint32_t sl = 0; sl < 4u * n; ++sl) {
+            const size_t base = (size_t)(sl / 4u) * 4u * kGroupF4 + sl % 4u;
+            gv[base + 4u * kRowR2P] = std::isfinite(gv[base + 4u * kRowR2P]) ? gv[base + 4u * kRowR2] : -INFINITY;
+        }
     return RT_OK;
 }
 
@@ -579,13 +597,15 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
     PackedSet ps[2];
     for (int rs = 0; rs < 2; ++rs) {
-        const int rc = pack_set(scene, rs, ps[rs]);
+        const int rc = pack_set(scene, rs, ps[rs], d->pf_rel_env);
         if (rc) return rc;
     }
     HIP_OK(hipSetDevice(d->ordinal));
     if (const int rc = quiesce(d)) return rc;
     for (int rs = 0; rs < 2; ++rs) {
-        d->prefilter[rs] = d->prefilter_env < 0 ? (ps[rs].prefilter_pays ? 1u : 0u) : (uint32_t)d->prefilter_env;
+        d->prefilter[rs] = d->prefilter_env < 0 ? ((ps[rs].prefilter_pays || ps[rs].relative) ? 1u : 0u)
+                                                : (uint32_t)d->prefilter_env;
+        d->pf_relative[rs] = ps[rs].relative ? 1u : 0u;
         d->fast_sqrt[rs] = ps[rs].fast_sqrt;
         const int rc = upload_set(d, rs, ps[rs].groups, ps[rs].mats, ps[rs].n_groups);
         if (rc) return rc;
@@ -623,7 +643,7 @@ extern "C" int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, f
     if (rc) return rc;
     const uint32_t n = 4u * p.n_groups;
     *out_count = n;
-    if (out_flags) *out_flags = (p.prefilter_pays ? 1u : 0u) | (p.fast_sqrt ? 2u : 0u);
+    if (out_flags) *out_flags = (p.prefilter_pays ? 1u : 0u) | (p.fast_sqrt ? 2u : 0u) | (p.relative ? 4u : 0u);
     if ((out_r2 || out_r2p) && capacity < n) return fail(RT_EINVAL, "rt_scene_prefilter: capacity %u < %u", capacity, n);
     for (uint32_t s = 0; s < n; ++s) {
         const size_t base = (size_t)(s / 4u) * 4u * kGroupF4 + s % 4u;
@@ -705,6 +725,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.band_index = desc->BandIndex;
     a.sec_threshold = d->sec_threshold;
     a.prefilter = d->prefilter[rs];
+    a.pf_relative = d->pf_relative[rs];
     a.fast_sqrt = d->fast_sqrt[rs];
     if (a.prefilter && d->n_cpairs[rs] &&
         (d->clusters_env == 2 || (d->clusters_env == 1 && d->n_groups[rs] <= kClAutoGroups))) {

@@ -29,7 +29,8 @@ constexpr uint32_t kClAutoGroups = 64;  // used by default up to this many (rt_h
 
 // HBM layout of an uploaded scene (per rule set):
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
-//               r2p = prefilter threshold of the secondary-ray sphere loop (rt_host.cpp)
+//               r2p = prefilter threshold of the secondary-ray sphere loop (rt_host.cpp);
+//               with pf_relative, r*r again (-inf: never hit) and the threshold is formed per lane
 //   materials : 4*n_groups x 2 float4 = {Color.xyz, Specular}, {Emissive.xyz, IOR} (32 B/sphere)
 // r*r is precomputed on the host with the same f32 multiply the reference
 // repeats per test (main.cpp:406), so it is bit-identical.
@@ -63,6 +64,7 @@ struct TraceArgs {
     uint32_t lut_in_lds;         // rsqrt table in the LDS image (else read from HBM: rtk_lut_in_lds)
     uint32_t fold_in_lds;        // running-mean weight table in the LDS image (else computed: rtk_fold_in_lds)
     uint32_t scene_in_lds;       // groups + materials copied into the LDS image (else read from HBM: GS kernels)
+    uint32_t pf_relative;        // prefilter: row 3 holds r^2 and the threshold is per lane (rt_kernel.hip kPfRel)
 };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,

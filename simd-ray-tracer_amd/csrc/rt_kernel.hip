@@ -439,8 +439,8 @@ __device__ __forceinline__ f2 pair_dist(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 
 // sphere is missed under both rule sets -- and only groups where some lane
 // fails that proof run the exact test.  A wave with any lane outside the
 // |D|^2 bound runs the exact loop instead.
-__device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 &T) {
-    f2 cx, cy, cz, cc, e;
+__device__ __forceinline__ f2 pair_prefilter(const RayPk &r, f2 sx, f2 sy, f2 sz, f2 &T, f2 &cc) {
+    f2 cx, cy, cz, e;
     asm("v_pk_add_f32 %[cx], %[sx], %[rx] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
         "v_pk_add_f32 %[cy], %[sy], %[ry] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
         "v_pk_add_f32 %[cz], %[sz], %[rz] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
@@ -492,13 +492,31 @@ __device__ __forceinline__ void recheck_pairs(const TraceArgs &a, const float4 *
     }
 }
 
+// Per-lane ("relative") prefilter threshold: t = RN(cc * 2^-15 + r^2) with
+// cc = the lane's computed |C|^2, where row 3 holds r^2 (-inf: never hit).
+// The error bound of e (and of the reference-rounded dist) scales with the
+// lane's own |C|^2 instead of the scene-wide M_j, so the test still proves
+// misses in scenes whose M_j bound is useless (RTWeekend's ground sphere
+// makes M ~ 1.6e4 against r^2 ~ 1.6e-4).  Proof: with
+// |C|^2 <= cc (1 + 5u) and E = 23.5u + K(1+K) the combined error of e and of
+// the reference's dist relative to |C|^2, e >= t gives dist > r^2 whenever
+// cc >= r^2 / 232 (then cc (2^-15 (1-u) - (1+5u) E) >= u r^2 covers t's own
+// rounding); and when cc < r^2 / 232, e <= cc < t, so nothing is skipped.
+constexpr float kPfRel = 0x1p-15f;
+
 // Prefilter flags of group G's two sphere pairs for this lane's ray.
+template <bool REL>
 __device__ __forceinline__ void prefilter_group(const Group &G, const RayPk &p, bool &f01, bool &f23) {
-    f2 T01, T23;
-    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
-    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
-    f01 = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]);
-    f23 = !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
+    f2 T01, T23, c01, c23;
+    const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01, c01);
+    const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23, c23);
+    if (REL) {
+        f01 = !(e01.x >= __builtin_fmaf(c01.x, kPfRel, G.r2p[0])) | !(e01.y >= __builtin_fmaf(c01.y, kPfRel, G.r2p[1]));
+        f23 = !(e23.x >= __builtin_fmaf(c23.x, kPfRel, G.r2p[2])) | !(e23.y >= __builtin_fmaf(c23.y, kPfRel, G.r2p[3]));
+    } else {
+        f01 = !(e01.x >= G.r2p[0]) | !(e01.y >= G.r2p[1]);
+        f23 = !(e23.x >= G.r2p[2]) | !(e23.y >= G.r2p[3]);
+    }
 }
 
 // Group g for a secondary ray through the prefilter: one wave branch per
@@ -508,17 +526,17 @@ struct PfStats {
     uint32_t groups, groups_noown, pairs, pairs_noown, lane_pairs;
 };
 
-template <bool SIMD, bool GS>
+template <bool SIMD, bool GS, bool REL>
 __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
                                               const RayPk &p, Hit &h, uint32_t own = ~0u, PfStats *ps = nullptr) {
     bool f01, f23;
-    prefilter_group(G, p, f01, f23);
+    prefilter_group<REL>(G, p, f01, f23);
     if (ps) {
         const bool mine = (own >> 2) == g;
         const uint32_t ol = own & 3u;
-        f2 T01, T23;
-        const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01);
-        const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23);
+        f2 T01, T23, c01, c23;
+        const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01, c01);
+        const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23, c23);
         const bool n01 = (!(e01.x >= G.r2p[0]) && !(mine && ol == 0u)) | (!(e01.y >= G.r2p[1]) && !(mine && ol == 1u));
         const bool n23 = (!(e23.x >= G.r2p[2]) && !(mine && ol == 2u)) | (!(e23.y >= G.r2p[3]) && !(mine && ol == 3u));
         ps->groups += __ballot(f01 | f23) != 0;
@@ -544,7 +562,7 @@ __device__ __forceinline__ Group load_group_pf_at(cv4f_t *cg) {
 
 // The full sphere loop over all groups from SGPRs.  PF: secondary rays
 // through the prefilter; else the exact test.
-template <bool SIMD, bool PF, bool GS>
+template <bool SIMD, bool PF, bool GS, bool REL = false>
 __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray, Hit &h,
                                                 uint32_t *hit_groups, uint32_t own = ~0u, PfStats *ps = nullptr) {
     cv4f_t *gp = (cv4f_t *)a.groups;
@@ -554,7 +572,7 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
     // measured 2 % slower)
     for (uint32_t g = 0; g < a.n_groups; ++g, gp += kGroupF4) {
         const Group G = PF ? load_group_pf_at(gp) : load_group_at(gp);
-        if (PF) test_group_pf<SIMD, GS>(a, lds_groups, G, g, ray, h, own, ps);
+        if (PF) test_group_pf<SIMD, GS, REL>(a, lds_groups, G, g, ray, h, own, ps);
         else test_group<SIMD>(a, G, g, ray, h, hit_groups);
     }
 }
@@ -585,8 +603,8 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         cv4f_t *e = ct + kClEntryF4 * m;
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];
-        f2 T;
-        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T);
+        f2 T, cc;
+        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
         // a lane may hit the sphere: near the line, and not wholly behind the origin
         const bool f0 = !(v.x >= r1.z) && !(T.x < r3.x), f1 = !(v.y >= r1.w) && !(T.y < r3.y);
         if (W == 1) {  // precomputed pair bits
@@ -611,8 +629,8 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         cv4f_t *e = ct + kClEntryF4 * c;
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];
-        f2 T;
-        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T);
+        f2 T, cc;
+        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
         const bool in0 = __ballot(!(v.x >= r1.z) && !(T.x < r3.x)) != 0;
         const bool in1 = __ballot(!(v.y >= r1.w) && !(T.y < r3.y)) != 0;
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
@@ -975,6 +993,10 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                             PfStats *ps = kStats && a.stats ? &st_pf : nullptr;
                             if (a.cl_words == 1u) clustered_groups<SIMD, 1, GS>(a, lds_groups, ray, h, ps);
                             else clustered_groups<SIMD, 2, GS>(a, lds_groups, ray, h, ps);
+                        } else if (SRC == kSrcSmem && pf && a.pf_relative) {
+                            if (kStats && a.stats) st_pf_rounds += 1;
+                            all_groups_smem<SIMD, true, GS, true>(a, lds_groups, ray, h, nullptr, p.own,
+                                                                  kStats && a.stats ? &st_pf : nullptr);
                         } else if (SRC == kSrcSmem && pf) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             all_groups_smem<SIMD, true, GS>(a, lds_groups, ray, h, nullptr, p.own,

@@ -6,7 +6,9 @@ and its behind-origin rule.  The built-in scenes exercise them
 only in one regime, so this generator builds scenes that stress the slack:
 - sphere counts from 1 to 1,060 (265 groups, the LDS-staged maximum);
 - radii log-uniform over 1e-3 ... 1e2 of a world scale itself drawn from
-  1e-2 ... 1e2 (so the reference's absolute eps = 1e-4 is met at every scale);
+  1e-2 ... 1e2 (so the reference's absolute eps = 1e-4 is met at every scale),
+  or, in "cloud" scenes, within one decade (the scene-wide prefilter bound
+  then pays, and the cluster walk runs);
 - overlapping, nested, near-coincident and near-tangent sphere pairs;
 - four cameras per scene: outside the cloud, inside a sphere, on a sphere's
   surface, and one with spheres placed tangent to film rays (grazing hits);
@@ -31,13 +33,20 @@ def make(seed: int, n_max: int = 1060):
     """Returns dict(spheres (N,20) f32, use_sky, cameras=[(look_at, distance, x_angle, y_height, kind)])."""
     rng = np.random.default_rng(seed)
     scale = float(10.0 ** rng.uniform(-2, 2))
-    # mostly small scenes (fast oracle), some large, one in eight at the maximum
-    n = int(rng.choice([rng.integers(1, 9), rng.integers(9, 80), rng.integers(80, 300), n_max],
-                       p=[0.25, 0.45, 0.2, 0.1]))
+    # "cloud" scenes (radii within one decade, like the built-in Floating Spheres)
+    # keep the scene-wide prefilter bound useful, so the cluster walk and its
+    # behind-origin rule run; "wide" scenes (radii over three decades, a huge
+    # sphere) take the per-lane thresholds
+    cloud = rng.random() < 0.4
+    if cloud:
+        n = int(rng.integers(8, 257))
+    else:  # mostly small scenes (fast oracle), some large, one in ten at the maximum
+        n = int(rng.choice([rng.integers(1, 9), rng.integers(9, 80), rng.integers(80, 300), n_max],
+                           p=[0.25, 0.45, 0.2, 0.1]))
     extent = scale * rng.uniform(1.0, 4.0)
     c = rng.uniform(-extent, extent, (n, 3))
-    r = scale * 10.0 ** rng.uniform(-3, 0, n)
-    if n > 4 and rng.random() < 0.3:  # one huge sphere (a ground, or a sphere around everything)
+    r = scale * (10.0 ** rng.uniform(np.log10(0.05), np.log10(0.3), n) if cloud else 10.0 ** rng.uniform(-3, 0, n))
+    if not cloud and n > 4 and rng.random() < 0.3:  # one huge sphere (a ground, or a sphere around everything)
         k = rng.integers(n)
         r[k] = scale * 10.0 ** rng.uniform(1, 2)
         if rng.random() < 0.5:
@@ -82,7 +91,7 @@ def make(seed: int, n_max: int = 1060):
     cams.append((c[k], float(np.float32(r[k])), ang, 0.0, "on_surface"))
     cams.append((centroid, float(extent * rng.uniform(1.5, 3.0)), float(rng.uniform(-6, 6)),
                  float(extent * rng.uniform(-0.3, 0.3)), "grazing"))
-    return {"spheres": sp, "use_sky": use_sky, "cameras": cams, "scale": scale, "n": n}
+    return {"spheres": sp, "use_sky": use_sky, "cameras": cams, "scale": scale, "n": n, "cloud": cloud}
 
 
 def add_grazing_spheres(rt, spec, W, H, count=4, seed=0):

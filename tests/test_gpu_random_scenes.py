@@ -2,8 +2,9 @@
 seeded scenes x 4 cameras (outside, inside a sphere, on a sphere, grazing
 spheres) x both rule sets, bit-exact against the oracle.  The kernel's
 proof-based skips -- the cone cull with its dead tiles, the secondary-ray
-prefilter, the cluster walk with the behind-origin rule -- run with their
-default per-scene choices, and the set must exercise every one of them."""
+prefilter (scene-wide or per-lane thresholds), the cluster walk with the
+behind-origin rule -- run with their default per-scene choices, and the set
+must exercise every one of them."""
 import numpy as np
 import pytest
 
@@ -13,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 SEEDS = list(range(56))
 W, H, S, B = 40, 24, 2, 6
-_seen = {"culled_groups": 0, "dead_tiles": 0, "prefilter": 0, "clusters": 0, "inside": 0}
+_seen = {"culled_groups": 0, "dead_tiles": 0, "prefilter": 0, "relative": 0, "clusters": 0, "inside": 0}
 
 
 @pytest.fixture(scope="module")
@@ -35,8 +36,10 @@ def test_random_scene_matches_oracle(rt, orc, torch_cuda, rdev, seed):
             rdev.upload_scene(s)
             first = False
             for simd in (True, False):
-                _seen["prefilter"] += rt.scene_prefilter(s, simd)[2] & 1
-                _seen["clusters"] += rt.scene_clusters(s, simd)[1] > 0
+                flags = rt.scene_prefilter(s, simd)[2]
+                _seen["prefilter"] += flags & 1
+                _seen["relative"] += (flags >> 2) & 1
+                _seen["clusters"] += (flags & 1) and rt.scene_clusters(s, simd)[1] > 0
         cam = rt.camera_setup(s, W, H)
         ocam = orc.camera(o, W, H)
         for simd in (True, False):

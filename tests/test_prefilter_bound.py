@@ -27,12 +27,25 @@ def exact_dist(cx, cy, cz, dx, dy, dz):
     return (qx * qx + qy * qy) + qz * qz
 
 
-def prefilter(cx, cy, cz, dx, dy, dz, with_t=False):
-    """rt_kernel.hip pair_prefilter, lane by lane: e (and its FMA T)."""
+def prefilter(cx, cy, cz, dx, dy, dz, with_t=False, with_cc=False):
+    """rt_kernel.hip pair_prefilter, lane by lane: e (and its FMA T, and cc = |C|^2)."""
     cc = fma(cx, cx, fma(cy, cy, cz * cz))
     T = fma(cz, dz, fma(cy, dy, cx * dx))
     e = fma(-T, T, cc)
+    if with_cc:
+        return e, T, cc
     return (e, T) if with_t else e
+
+
+PF_REL = F(2.0 ** -15)  # rt_kernel.hip kPfRel
+
+
+def threshold(r2p, cc, relative):
+    """The kernel's skip threshold: r2p (scene-wide), or RN(cc 2^-15 + r^2) per lane."""
+    if not relative:
+        return r2p
+    with np.errstate(invalid="ignore"):
+        return fma(cc, np.broadcast_to(PF_REL, cc.shape), np.broadcast_to(r2p, cc.shape))
 
 
 def could_accept(cx, cy, cz, dx, dy, dz, r2, simd):
@@ -113,14 +126,17 @@ def check_prefilter(rt, scene, simd, seed, n_rays=4000, require_hits=True):
     cz = centres[None, :, 2] - o[:, None, 2]
     dx, dy, dz = d[:, None, 0], d[:, None, 1], d[:, None, 2]
     dist = exact_dist(cx, cy, cz, dx, dy, dz)
-    e = prefilter(cx, cy, cz, dx, dy, dz)
+    e, _, cc = prefilter(cx, cy, cz, dx, dy, dz, with_cc=True)
     hit = (dist < r2) if simd else ~(dist > r2)
     hit &= live[None, :]
-    skipped = ~(e < r2p)
+    relative = bool(flags & 4)
+    skipped = ~(e < threshold(r2p[None, :], cc, relative))
     assert not np.any(hit & skipped), "prefilter skipped a sphere the exact test accepts"
     if require_hits:
         assert hit.sum() > 0
-    return bool(flags & 1), int((skipped & live[None, :]).sum())
+    if relative and require_hits:  # the per-lane threshold must cull too
+        assert (~skipped & live[None, :]).sum() < 1.5 * hit.sum() + 0.2 * live.sum() * len(o)
+    return bool(flags & 5), int((skipped & live[None, :]).sum())
 
     if flags & 1 and require_hits:  # where it is enabled, the prefilter must actually cull
         assert (~skipped).sum() < 1.5 * hit.sum() + 0.05 * hit.size

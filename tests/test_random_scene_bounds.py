@@ -46,7 +46,24 @@ def test_random_scene_bounds(rt, orc, seed):
                         assert (words[gi // 64] >> (gi % 64)) & 1, f"{kind}: pixel ({x},{y}) reaches group {gi}"
 
 
-def test_random_scenes_exercise_every_skip():
-    if not _seen["prefilter_on"]:
-        pytest.skip("run with the per-seed tests")
-    assert all(v > 0 for v in _seen.values()), _seen
+def test_random_scenes_exercise_every_skip(rt, orc):
+    """Over the seed set, every proof-based skip actually fires somewhere (counted
+    afresh here, so the test does not depend on the per-seed tests' process)."""
+    seen = dict.fromkeys(_seen, 0)
+    for seed in SEEDS:
+        spec = random_scenes.make(seed)
+        look, dist, ang, yh, _ = spec["cameras"][0]
+        scene, _ = random_scenes.build(rt, orc, spec["spheres"], spec["use_sky"], look, dist, ang, yh)
+        for simd in (True, False):
+            on, culled = check_prefilter(rt, scene, simd, seed, n_rays=300, require_hits=False)
+            seen["prefilter_on"] += on
+            seen["prefilter_culls"] += culled > 0
+            sk, bh = check_clusters(rt, scene, simd, seed, n_rays=300)
+            seen["cluster_skips"] += sk > 0
+            seen["behind_skips"] += bh > 0
+        cam = rt.camera_setup(scene, 24, 16)
+        masks = np_masks(rt, scene, cam, 24, 16, 4)
+        ng = scene_spheres(rt, scene)[2]
+        nw = (ng + 63) // 64
+        seen["cull_culls"] += sum(bin(int(v)).count("1") for v in masks) < (len(masks) // nw) * ng
+    assert all(v > 0 for v in seen.values()), seen
