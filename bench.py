@@ -378,9 +378,13 @@ def main():
 
     if bands != world:
         if rank == 0:
-            print(json.dumps({"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
-                              "rank0_kernel_ms": round(kern_ms, 3), "lanes_per_pixel": info["LanesPerPixel"],
-                              "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}))
+            out = {"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
+                   "rank0_kernel_ms": round(kern_ms, 3), "lanes_per_pixel": info["LanesPerPixel"],
+                   "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}
+            stats = dev.debug_stats()
+            if stats:
+                out["sched_stats"] = stats
+            print(json.dumps(out))
         if comm:
             comm.close()
         dev.close()

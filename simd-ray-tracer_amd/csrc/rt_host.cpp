@@ -46,6 +46,7 @@ struct rt_device {
     int clusters_env = 1;
     int interleave_env = 0;  // RT_INTERLEAVE=1: wave tiles interleaved over the block tile (P >= 2)
     int scene_global_env = 0;  // RT_SCENE_GLOBAL=1: keep the scene in HBM even when the LDS image could hold it
+    int tables_global_env = 0;  // RT_TABLES_LDS=0: the rsqrt and fold-weight tables stay out of the LDS image
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
@@ -145,6 +146,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (il && (il[0] == '0' || il[0] == '1')) d->interleave_env = il[0] - '0';
     const char *sg = getenv("RT_SCENE_GLOBAL");
     if (sg && sg[0] == '1') d->scene_global_env = 1;
+    const char *tl = getenv("RT_TABLES_LDS");  // 0: rsqrt + fold tables read through the caches at every size (A/B)
+    if (tl && tl[0] == '0') d->tables_global_env = 1;
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -768,8 +771,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         a.wave_times = d->d_wave_times;
     }
     a.interleave = d->interleave_env && lpp >= 2 ? 1u : 0u;
-    a.lut_in_lds = rtk_lut_in_lds(a.n_groups) ? 1u : 0u;
-    a.fold_in_lds = rtk_fold_in_lds(a.n_groups) ? 1u : 0u;
+    a.lut_in_lds = rtk_lut_in_lds(a.n_groups) && !d->tables_global_env ? 1u : 0u;
+    a.fold_in_lds = rtk_fold_in_lds(a.n_groups) && !d->tables_global_env ? 1u : 0u;
     a.scene_in_lds = a.n_groups <= kMaxLdsGroups && !d->scene_global_env ? 1u : 0u;
     const int src = a.scene_in_lds ? d->src : kSrcSmem;  // a scene in HBM is read through the scalar cache
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
