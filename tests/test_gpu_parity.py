@@ -515,3 +515,25 @@ def test_scene_above_the_limit_is_refused(rt, torch_cuda, gdev):
     sp[:, 4] = 0.1
     with pytest.raises(rt.RtError, match="exceed"):
         gdev.upload_scene(rt.scene_from_spheres(sp))
+
+
+def test_probe_launch_changes_no_bit(rt, orc, torch_cuda, monkeypatch):
+    """The first launch of a key (frames >= 16 P) is preceded by a probe launch
+    into scratch images that measures tile costs for a heaviest-first order:
+    the frame, the accumulation and the ray count equal those of the launch
+    without it (RT_PROBE=0), and the oracle's."""
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", "4")
+    s, o = _scenes(rt, orc, 1, 64)
+    W, H, S, B = 192, 128, 64, 8
+    cam = rt.camera_setup(s, W, H)
+    out = []
+    for probe in ("0", "1"):
+        monkeypatch.setenv("RT_PROBE", probe)
+        dev = rt.Device(0)
+        try:
+            out.append(gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=S, bounces=B))
+        finally:
+            dev.close()
+    assert torch_cuda.equal(out[0][0], out[1][0]) and torch_cuda.equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
+    r = orc.render(o, orc.camera(o, W, H), W, H, frames=S, max_bounce=B, threads=orc.cpu_threads())
+    assert_same(*out[1], *r)
