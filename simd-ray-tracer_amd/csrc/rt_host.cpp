@@ -314,10 +314,27 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
 // mask in group order.  Returns the number of cluster-pair entries (0: not
 // used -- more than kClMaxGroups groups, too few hittable spheres); *words =
 // u64 words of the pair mask.
+//
+// relative (the per-lane thresholds of pack_set, where the scene-wide M makes
+// the bound above useless): the thresholds are formed per lane from the lane's
+// own cc = |Q|^2 (rt_kernel.hip kClRel / kPfRel / kBehindRel).  With A_j =
+// |Q|(1+u) + delta_j >= |C_j| (delta_j = |s_j - q_c|) the chain above reads
+//   sqrt(l(O+Q)) > delta_j + sqrt(r_j^2 + 13.3u A_j^2) + 2u A_j + u|Q|
+// and sqrt(r^2 + 13.3u A^2) <= r + sqrt(13.3u) A, so it holds when
+//   sqrt(l(O+Q)) > rho_j + a|Q|,  rho_j = delta_j (1+s) + r_j,  s = sqrt(13.3u) + 2u,  a = s(1+u) + u;
+// (rho + a|Q|)^2 <= rho^2 (1+a) + |Q|^2 (a + a^2), l(O+Q) >= e_c - E1 |Q|^2
+// (E1 = 10.2u + K(1+K)/(1-K)) and |Q|^2 <= cc (1 + 5.1u), so the cluster is
+// skipped when e_c >= RN(cc kClRel + R_c), R_c = rho_c^2 (1+a) rounded up,
+// kClRel >= (a + a^2 + E1)(1 + 6u) (both inflated for the FMA's rounding).
+// Members carry r^2 (the group rows' per-lane rule), behind thresholds lose
+// their M terms (|Q|, |C_j| <= (1 + cc)/2 bound them per lane, kBehindRel):
+//   cluster  -(max_j ((delta_j + r_j)(1 + 2^-15) + 4.3u delta_j) + 4.3u),
+//   member   -(r_j (1 + 2^-15) + 4.3u),
+// and a lane's behind test is T < RN(stored - 4.5u cc).
 static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, std::vector<float> &tab,
-                              uint32_t *words) {
+                              uint32_t *words, bool relative = false) {
     tab.clear();
-    *words = n_groups <= 32u ? 1u : 2u;
+    *words = n_groups <= 32u ? 1u : n_groups <= 64u ? 2u : 4u;
     if (n_groups > kClMaxGroups) return 0;
     struct Sph {
         uint32_t s;
@@ -341,8 +358,12 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         return (reach * 1.001 + 1e-3) * (reach * 1.001 + 1e-3);
     };
     const double u = 0x1p-24, K = 0x1p-16;
-    for (Sph &o : sp) o.m = bound_m(o.x, o.y, o.z);
-    auto sigma = [&](const Sph &o) { return std::sqrt(o.r * o.r + 13.3 * u * o.m) + u * std::sqrt(o.m); };
+    if (!relative)
+        for (Sph &o : sp) o.m = bound_m(o.x, o.y, o.z);
+    auto sigma = [&](const Sph &o) {
+        return relative ? o.r : std::sqrt(o.r * o.r + 13.3 * u * o.m) + u * std::sqrt(o.m);
+    };
+    const double s_rel = std::sqrt(13.3 * u) + 2.0 * u, a_rel = s_rel * (1.0 + u) + u;
     // max(1.25 sqrt(n), n/8) clusters: measured on C2 (N = 64) K = 6/8/10/12/16 ->
     // 112.4k/113.8k/114.6k/114.5k/111.4k Mrays/s; at 200 spheres K = 17/28 ->
     // 45.0k/46.9k; at C5 (256) K = 20/26/32/40 -> 30.1k/31.3k/32.4k/32.4k
@@ -434,7 +455,8 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // under the |D|^2 bound).  Per sphere (q_c = S_j): b_j = r_j(1 + 2^-15) + 8.6u sqrt(M_j).
     std::vector<float> beta_of_slot(4u * n_groups, 0.0f);
     for (const Sph &o : sp)
-        beta_of_slot[o.s] = std::nextafter((float)-(o.r * (1.0 + 0x1p-15) + 8.6 * u * std::sqrt(o.m)), -INFINITY);
+        beta_of_slot[o.s] = relative ? std::nextafter((float)(-(o.r * (1.0 + 0x1p-15) + 4.3 * u) * (1.0 + 1e-6)), -INFINITY)
+                                     : std::nextafter((float)-(o.r * (1.0 + 0x1p-15) + 8.6 * u * std::sqrt(o.m)), -INFINITY);
     for (uint32_t c = 0; c < k; ++c) {
         Cl C;
         double sx = 0.0, sy = 0.0, sz = 0.0;
@@ -450,19 +472,29 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         C.qy = (float)(sy / C.mem.size());
         C.qz = (float)(sz / C.mem.size());
         const double qx = C.qx, qy = C.qy, qz = C.qz;
-        double rho = 0.0;
-        for (uint32_t i : C.mem)
-            rho = std::max(rho, std::sqrt((sp[i].x - qx) * (sp[i].x - qx) + (sp[i].y - qy) * (sp[i].y - qy) +
-                                          (sp[i].z - qz) * (sp[i].z - qz)) + sigma(sp[i]));
-        const double mc = bound_m(qx, qy, qz);
-        rho = (rho + u * std::sqrt(mc)) * (1.0 + 1e-6);
-        C.t = std::nextafter((float)(rho * rho + mc * (32.0 * u + 1.01 * K)), INFINITY);
-        double bmax = 0.0;
-        for (uint32_t i : C.mem)
-            bmax = std::max(bmax, (std::sqrt((sp[i].x - qx) * (sp[i].x - qx) + (sp[i].y - qy) * (sp[i].y - qy) +
-                                             (sp[i].z - qz) * (sp[i].z - qz)) + sp[i].r) * (1.0 + 0x1p-15) +
-                                      4.3 * u * (std::sqrt(mc) + std::sqrt(sp[i].m)));
-        C.b = std::nextafter((float)-bmax, -INFINITY);
+        auto delta = [&](uint32_t i) {
+            return std::sqrt((sp[i].x - qx) * (sp[i].x - qx) + (sp[i].y - qy) * (sp[i].y - qy) +
+                             (sp[i].z - qz) * (sp[i].z - qz));
+        };
+        if (relative) {
+            double rho = 0.0, bmax = 0.0;
+            for (uint32_t i : C.mem) {
+                rho = std::max(rho, delta(i) * (1.0 + s_rel) + sp[i].r);
+                bmax = std::max(bmax, (delta(i) + sp[i].r) * (1.0 + 0x1p-15) + 4.3 * u * delta(i));
+            }
+            C.t = std::nextafter((float)(rho * rho * (1.0 + a_rel) * (1.0 + 1e-6)), INFINITY);
+            C.b = std::nextafter((float)(-(bmax + 4.3 * u) * (1.0 + 1e-6)), -INFINITY);
+        } else {
+            double rho = 0.0;
+            for (uint32_t i : C.mem) rho = std::max(rho, delta(i) + sigma(sp[i]));
+            const double mc = bound_m(qx, qy, qz);
+            rho = (rho + u * std::sqrt(mc)) * (1.0 + 1e-6);
+            C.t = std::nextafter((float)(rho * rho + mc * (32.0 * u + 1.01 * K)), INFINITY);
+            double bmax = 0.0;
+            for (uint32_t i : C.mem)
+                bmax = std::max(bmax, (delta(i) + sp[i].r) * (1.0 + 0x1p-15) + 4.3 * u * (std::sqrt(mc) + std::sqrt(sp[i].m)));
+            C.b = std::nextafter((float)-bmax, -INFINITY);
+        }
         for (uint32_t &i : C.mem) i = sp[i].s;
         cl.push_back(std::move(C));
     }
@@ -476,7 +508,10 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         const uint32_t g = (s / 4u) * 4u * kGroupF4, l = s % 4u;
         return gv[g + 4u * (uint32_t)axis + l];
     };
-    auto sphere_r2p = [&](uint32_t s) { return gv[(s / 4u) * 4u * kGroupF4 + 4u * kRowR2P + s % 4u]; };
+    // member threshold: the scene-wide r2p, or r^2 for the per-lane rule
+    auto sphere_r2p = [&](uint32_t s) {
+        return gv[(s / 4u) * 4u * kGroupF4 + 4u * (relative ? kRowR2 : kRowR2P) + s % 4u];
+    };
     uint32_t next = n_cp;
     for (uint32_t p = 0; p < n_cp; ++p) {
         float *e = &tab[(size_t)p * kClEntryF4 * 4u];
@@ -585,15 +620,12 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
     }
     p.prefilter_pays = prefilter_rows(gv, n, rs == 0);
     p.fast_sqrt = sqrt_range_ok(gv, n, rs == 0);
-    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words);  // (member rows keep the scene-wide r2p)
     // Where the scene-wide bound M_j makes r2p useless (a huge sphere: RTWeekend's
-    // ground), the per-group loop forms its threshold per lane from the lane's own
-    // |C|^2 instead (rt_kernel.hip kPfRel): row 3 then holds r^2 (-inf: never hit).
+    // ground), the thresholds are formed per lane from the lane's own |C|^2 instead
+    // (rt_kernel.hip kPfRel, kClRel): the cluster table is built for that rule, and
+    // row 3 then holds r^2 (-inf: never hit).
     p.relative = pf_rel_env == 1 || (pf_rel_env < 0 && !p.prefilter_pays);
-    if (p.relative) {  // (the cluster table's scene-wide thresholds would not pay either)
-        p.n_cpairs = 0;
-        p.clusters.clear();
-    }
+    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words, p.relative);
     if (p.relative)
         for (uint32_t sl = 0; sl < 4u * n; ++sl) {
             const size_t base = (size_t)(sl / 4u) * 4u * kGroupF4 + sl % 4u;
@@ -777,8 +809,12 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         a.wave_times = d->d_wave_times;
     }
     a.interleave = d->interleave_env && lpp >= 2 ? 1u : 0u;
-    a.lut_in_lds = rtk_lut_in_lds(a.n_groups) && !d->tables_global_env ? 1u : 0u;
-    a.fold_in_lds = rtk_fold_in_lds(a.n_groups) && !d->tables_global_env ? 1u : 0u;
+    // The rsqrt and fold tables (10 KB) leave the LDS image at P = 16, whose 4-wave
+    // ring (10 KB) would otherwise cap a CU at 6 blocks: measured on the 8-rank C2
+    // share 0.900-0.903 against 0.914-0.922 ms; at P = 4 they stay (C2 -1.8 % without)
+    const bool tables = !d->tables_global_env && lpp <= 8;
+    a.lut_in_lds = rtk_lut_in_lds(a.n_groups) && tables ? 1u : 0u;
+    a.fold_in_lds = rtk_fold_in_lds(a.n_groups) && tables ? 1u : 0u;
     a.scene_in_lds = a.n_groups <= kMaxLdsGroups && !d->scene_global_env ? 1u : 0u;
     const int src = a.scene_in_lds ? d->src : kSrcSmem;  // a scene in HBM is read through the scalar cache
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);

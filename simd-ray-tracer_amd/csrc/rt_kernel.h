@@ -21,11 +21,13 @@ enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // is its sphere pair in group order, the bit it sets in the wave's pair mask).
 // The wave mask is kept in SGPRs, cl_words u64 words of it:
 //   1 (n_groups <= 32): bits = {lo, hi of 1 << q for member 0, the same for member 1}
-//   2 (n_groups <= 64): bits = {q0, q1, 0, 0}
+//   2 (n_groups <= 64), 4 (n_groups <= 128): bits = {q0, q1, 0, 0}
+// With pf_relative the thresholds are per lane: rc2p / r2p hold R_c / r^2 and
+// b the M-free behind bases (rt_host.cpp cluster_table, "relative").
 // padding members: threshold -inf, bits 0 / q = 0xFFFFFFFF.
 constexpr uint32_t kClEntryF4 = 4;
-constexpr uint32_t kClMaxGroups = 64;   // table built up to this many groups
-constexpr uint32_t kClAutoGroups = 64;  // used by default up to this many (rt_host.cpp clusters_env)
+constexpr uint32_t kClMaxGroups = 128;   // table built up to this many groups
+constexpr uint32_t kClAutoGroups = 128;  // used by default up to this many (rt_host.cpp clusters_env)
 
 // HBM layout of an uploaded scene (per rule set):
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)

@@ -588,16 +588,23 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // come out as in the full loop.  The recheck runs on every lane: a lane whose
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
+constexpr int kClWords = 4;  // pair-mask words (n_groups <= 128)
 template <int W>
-__device__ __forceinline__ void set_pair(uint64_t (&wave)[2], bool any, uint32_t q) {  // W = 2: pair index q
+__device__ __forceinline__ void set_pair(uint64_t (&wave)[kClWords], bool any, uint32_t q) {  // W >= 2: pair index q
     const uint64_t bit = any ? 1ull << (q & 63u) : 0ull;  // padding (q = ~0) never has any
-    wave[0] |= q < 64u ? bit : 0ull;
-    wave[1] |= q < 64u ? 0ull : bit;
+#pragma unroll
+    for (int w = 0; w < W; ++w) wave[w] |= (q >> 6) == (uint32_t)w ? bit : 0ull;
 }
 
-template <int W>
+// Per-lane thresholds (pf_relative, rt_host.cpp cluster_table "relative"):
+// cluster: e_c >= RN(cc kClRel + R_c); sphere: e >= RN(cc kPfRel + r^2) (kPfRel
+// below); behind: T < RN(b - cc kBehindRel).
+constexpr float kClRel = 9.2e-4f;               // >= (a + a^2 + E1)(1 + 6u), a = 8.917e-4
+constexpr float kBehindRel = 4.5f * 0x1p-24f;    // >= 4.3u (|Q|, |C_j| <= (1 + cc)/2)
+
+template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
-                                             uint64_t (&wave)[2], PfStats *ps) {
+                                             uint64_t (&wave)[kClWords], PfStats *ps) {
     if (ps) ps->groups += count;
     for (uint32_t m = first; m < first + count; ++m) {
         cv4f_t *e = ct + kClEntryF4 * m;
@@ -606,7 +613,11 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         f2 T, cc;
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
         // a lane may hit the sphere: near the line, and not wholly behind the origin
-        const bool f0 = !(v.x >= r1.z) && !(T.x < r3.x), f1 = !(v.y >= r1.w) && !(T.y < r3.y);
+        const float t0 = REL ? __builtin_fmaf(cc.x, kPfRel, r1.z) : r1.z;
+        const float t1 = REL ? __builtin_fmaf(cc.y, kPfRel, r1.w) : r1.w;
+        const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
+        const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
+        const bool f0 = !(v.x >= t0) && !(T.x < b0), f1 = !(v.y >= t1) && !(T.y < b1);
         if (W == 1) {  // precomputed pair bits
             const uint64_t b0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
             const uint64_t b1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
@@ -620,22 +631,26 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
 
 // ps (RTK_STATS): groups += member-pair entries tested, pairs += sphere pairs
 // rechecked exactly, lane_pairs += clusters entered (per wave).
-template <bool SIMD, int W, bool GS>
+template <bool SIMD, int W, bool GS, bool REL>
 __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray,
                                                  Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
-    uint64_t wave[2] = {0ull, 0ull};
+    uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
     for (uint32_t c = 0; c < a.n_cpairs; ++c) {
         cv4f_t *e = ct + kClEntryF4 * c;
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];
         f2 T, cc;
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
-        const bool in0 = __ballot(!(v.x >= r1.z) && !(T.x < r3.x)) != 0;
-        const bool in1 = __ballot(!(v.y >= r1.w) && !(T.y < r3.y)) != 0;
+        const float t0 = REL ? __builtin_fmaf(cc.x, kClRel, r1.z) : r1.z;
+        const float t1 = REL ? __builtin_fmaf(cc.y, kClRel, r1.w) : r1.w;
+        const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
+        const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
+        const bool in0 = __ballot(!(v.x >= t0) && !(T.x < b0)) != 0;
+        const bool in1 = __ballot(!(v.y >= t1) && !(T.y < b1)) != 0;
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
-        if (in0) member_pairs<W>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
-        if (in1) member_pairs<W>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);
+        if (in0) member_pairs<W, REL>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
+        if (in1) member_pairs<W, REL>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);
     }
     cv4f_t *gp = (cv4f_t *)a.groups;
 #pragma unroll
@@ -991,8 +1006,15 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         if (SRC == kSrcSmem && pf && a.n_cpairs) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             PfStats *ps = kStats && a.stats ? &st_pf : nullptr;
-                            if (a.cl_words == 1u) clustered_groups<SIMD, 1, GS>(a, lds_groups, ray, h, ps);
-                            else clustered_groups<SIMD, 2, GS>(a, lds_groups, ray, h, ps);
+                            if (a.pf_relative) {
+                                if (a.cl_words == 1u) clustered_groups<SIMD, 1, GS, true>(a, lds_groups, ray, h, ps);
+                                else if (a.cl_words == 2u) clustered_groups<SIMD, 2, GS, true>(a, lds_groups, ray, h, ps);
+                                else clustered_groups<SIMD, 4, GS, true>(a, lds_groups, ray, h, ps);
+                            } else {
+                                if (a.cl_words == 1u) clustered_groups<SIMD, 1, GS, false>(a, lds_groups, ray, h, ps);
+                                else if (a.cl_words == 2u) clustered_groups<SIMD, 2, GS, false>(a, lds_groups, ray, h, ps);
+                                else clustered_groups<SIMD, 4, GS, false>(a, lds_groups, ray, h, ps);
+                            }
                         } else if (SRC == kSrcSmem && pf && a.pf_relative) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             all_groups_smem<SIMD, true, GS, true>(a, lds_groups, ray, h, nullptr, p.own,

@@ -40,6 +40,26 @@ def prefilter(cx, cy, cz, dx, dy, dz, with_t=False, with_cc=False):
 PF_REL = F(2.0 ** -15)  # rt_kernel.hip kPfRel
 
 
+CL_REL = F(9.2e-4)            # rt_kernel.hip kClRel
+BEHIND_REL = F(4.5 * 2.0 ** -24)  # rt_kernel.hip kBehindRel
+
+
+def cluster_threshold(t, cc, relative):
+    """Cluster skip threshold: the stored rc2p, or RN(cc kClRel + R_c) per lane."""
+    if not relative:
+        return t
+    with np.errstate(invalid="ignore"):
+        return fma(cc, np.broadcast_to(CL_REL, cc.shape), np.broadcast_to(F(t), cc.shape))
+
+
+def behind_threshold(b, cc, relative):
+    """Behind threshold: the stored b, or RN(b - cc kBehindRel) per lane."""
+    if not relative:
+        return b
+    with np.errstate(invalid="ignore"):
+        return fma(cc, np.broadcast_to(-BEHIND_REL, cc.shape), np.broadcast_to(b, cc.shape))
+
+
 def threshold(r2p, cc, relative):
     """The kernel's skip threshold: r2p (scene-wide), or RN(cc 2^-15 + r^2) per lane."""
     if not relative:
@@ -159,7 +179,7 @@ def test_short_sqrt_flag_follows_the_radius_range(rt):
     assert not rt.scene_prefilter(tiny, True)[2] & 2 and not rt.scene_prefilter(tiny, False)[2] & 2
 
 
-@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 37), (1, 16), (1, 100), (1, 256), (0, None)])
+@pytest.mark.parametrize("idx,n_spheres", [(1, 64), (1, 37), (1, 16), (1, 100), (1, 256), (0, None), (2, None)])
 @pytest.mark.parametrize("simd", [True, False])
 def test_cluster_prefilter_never_skips_an_exact_hit(rt, idx, n_spheres, simd):
     """The clustered loop (rt_kernel.hip clustered_groups) skips every member
@@ -179,9 +199,10 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
     rule) and no skipped member holds a sphere a lane can accept.  Returns
     (rays x clusters skipped, of them by the behind rule)."""
     tab, ncp = rt.scene_clusters(scene, simd)
-    r2, r2p, _ = rt.scene_prefilter(scene, simd)
+    r2, r2p, flags = rt.scene_prefilter(scene, simd)
     if ncp == 0:
         return 0, 0
+    relative = bool(flags & 4)  # per-lane thresholds (rt_kernel.hip kClRel / kPfRel / kBehindRel)
     centres, radius = slot_spheres(rt, scene, simd)
     live = np.isfinite(r2p)
     # decode the table: clusters -> member spheres (by centre and r2p) and pair indices
@@ -231,22 +252,25 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
     if require_culls:
         assert accept.sum() > 0
     # sphere level: near-line estimate or wholly behind the origin (member rows)
-    e_s, t_s = prefilter(cx, cy, cz, dx, dy, dz, with_t=True)
+    e_s, t_s, cc_s = prefilter(cx, cy, cz, dx, dy, dz, with_cc=True)
     beta = np.array([beta_of.get(k, -np.inf) for k in range(len(r2))], F)
-    skip_s = ~(e_s < r2p[None, :]) | (t_s < beta[None, :])
+    thr_s = threshold(r2p[None, :], cc_s, relative)
+    beta_s = behind_threshold(beta[None, :], cc_s, relative)
+    skip_s = ~(e_s < thr_s) | (t_s < beta_s)
     assert not np.any(accept & skip_s), "the member test skipped a sphere a lane can accept"
     if require_culls:
-        assert np.any((t_s < beta[None, :]) & (e_s < r2p[None, :]) & live[None, :]), "the behind rule culls nothing"
+        assert np.any((t_s < beta_s) & (e_s < thr_s) & live[None, :]), "the behind rule culls nothing"
     skipped_any = behind_any = 0
     for qx, qy, qz, t, ms, bc in members:
         if np.isneginf(t):
             continue
-        ex, tx = prefilter((qx - o[:, 0])[:, None], (qy - o[:, 1])[:, None], (qz - o[:, 2])[:, None],
-                           d[:, 0:1], d[:, 1:2], d[:, 2:3], with_t=True)
-        behind = tx[:, 0] < bc
-        skip = ~(ex[:, 0] < t) | behind
+        ex, tx, cq = prefilter((qx - o[:, 0])[:, None], (qy - o[:, 1])[:, None], (qz - o[:, 2])[:, None],
+                               d[:, 0:1], d[:, 1:2], d[:, 2:3], with_cc=True)
+        tc = cluster_threshold(t, cq[:, 0], relative)
+        behind = tx[:, 0] < behind_threshold(bc, cq[:, 0], relative)
+        skip = ~(ex[:, 0] < tc) | behind
         skipped_any += int(skip.sum())
-        behind_any += int((behind & (ex[:, 0] < t)).sum())
+        behind_any += int((behind & (ex[:, 0] < tc)).sum())
         assert not np.any(accept[skip][:, ms]), "a skipped cluster holds a sphere a lane can accept"
     if require_culls:
         assert skipped_any > 0 and behind_any > 0  # both cluster rules cull
