@@ -72,7 +72,7 @@ enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriG
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
        kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatPfRounds, kStatPfGroups,
        kStatPfGroupsNoOwn, kStatPfPairs, kStatPfPairsNoOwn, kStatPfLanePairs, kStatPriBlocked, kStatPriWaitSec,
-       kStatPriDone, kStatCount = 25 };
+       kStatPriDone, kStatSecDone, kStatSecWaitPri, kStatDoneTrips, kStatDoneLaneTrips, kStatCount = 29 };
 constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 
 // Dynamic LDS per block: [rsqrt table] + fold table + groups + materials.

@@ -602,6 +602,13 @@ __device__ __forceinline__ void set_pair(uint64_t (&wave)[kClWords], bool any, u
 constexpr float kClRel = 9.2e-4f;               // >= (a + a^2 + E1)(1 + 6u), a = 8.917e-4
 constexpr float kBehindRel = 4.5f * 0x1p-24f;    // >= 4.3u (|Q|, |C_j| <= (1 + cc)/2)
 
+// ballot(a && b) as ballot(a) & ballot(b): the backend folds the ballot of a
+// single compare into the v_cmp's own lane mask, but materialises the ballot of
+// a conjunction through v_cndmask + v_cmp_ne (two VALU per ballot)
+__device__ __forceinline__ uint64_t ballot_and(bool a, bool b) {
+    return __builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b);
+}
+
 template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
                                              uint64_t (&wave)[kClWords], PfStats *ps) {
@@ -617,14 +624,15 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         const float t1 = REL ? __builtin_fmaf(cc.y, kPfRel, r1.w) : r1.w;
         const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-        const bool f0 = !(v.x >= t0) && !(T.x < b0), f1 = !(v.y >= t1) && !(T.y < b1);
+        const bool f0 = ballot_and(!(v.x >= t0), !(T.x < b0)) != 0;
+        const bool f1 = ballot_and(!(v.y >= t1), !(T.y < b1)) != 0;
         if (W == 1) {  // precomputed pair bits
             const uint64_t b0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
             const uint64_t b1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
-            wave[0] |= (__ballot(f0) != 0 ? b0 : 0ull) | (__ballot(f1) != 0 ? b1 : 0ull);
+            wave[0] |= (f0 ? b0 : 0ull) | (f1 ? b1 : 0ull);
         } else {
-            set_pair<W>(wave, __ballot(f0) != 0, __float_as_uint(r2.x));
-            set_pair<W>(wave, __ballot(f1) != 0, __float_as_uint(r2.y));
+            set_pair<W>(wave, f0, __float_as_uint(r2.x));
+            set_pair<W>(wave, f1, __float_as_uint(r2.y));
         }
     }
 }
@@ -646,8 +654,8 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         const float t1 = REL ? __builtin_fmaf(cc.y, kClRel, r1.w) : r1.w;
         const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-        const bool in0 = __ballot(!(v.x >= t0) && !(T.x < b0)) != 0;
-        const bool in1 = __ballot(!(v.y >= t1) && !(T.y < b1)) != 0;
+        const bool in0 = ballot_and(!(v.x >= t0), !(T.x < b0)) != 0;
+        const bool in1 = ballot_and(!(v.y >= t1), !(T.y < b1)) != 0;
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
         if (in0) member_pairs<W, REL>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
         if (in1) member_pairs<W, REL>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);
@@ -896,6 +904,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
     uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
     uint32_t st_pri_blocked = 0, st_pri_waitsec = 0, st_pri_done = 0;
+    uint32_t st_sec_done = 0, st_sec_waitpri = 0, st_done_trips = 0, st_done_lanes = 0;
     uint64_t st_cyc_pri = 0, st_cyc_sec = 0, st_cyc_fold = 0, st_cyc_setup = 0;
     uint64_t st_cyc_cull = 0, st_cyc_sync = 0, st_cyc_post = 0;
     PfStats st_pf = {0, 0, 0, 0, 0};
@@ -964,6 +973,13 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 if (do_sec && __builtin_popcountll(sec) < 16) { st_sparse_it += 1; st_sparse_lanes += __builtin_popcountll(sec); }
                 if (do_sec && __ballot(mode == 0u) == 0) st_tail_it += 1;  // no lane has a sample to start
+                if (do_sec) {  // a secondary round: where the other lanes are
+                    st_sec_done += __builtin_popcountll(__ballot(mode == 2u));
+                    st_sec_waitpri += __builtin_popcountll(__ballot(mode == 0u));
+                }
+                // trips with finished pixels (every sample started and traced) beside live ones
+                const uint32_t nd = __builtin_popcountll(__ballot(mode == 2u));
+                if (nd) { st_done_trips += 1; st_done_lanes += nd; }
                 if (!do_sec) {  // a primary round: where the other lanes are
                     st_pri_it += 1;
                     st_pri_lanes += __builtin_popcountll(pri);
@@ -1186,6 +1202,10 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatPriBlocked, (unsigned long long)st_pri_blocked);
         atomicAdd(a.stats + kStatPriWaitSec, (unsigned long long)st_pri_waitsec);
         atomicAdd(a.stats + kStatPriDone, (unsigned long long)st_pri_done);
+        atomicAdd(a.stats + kStatSecDone, (unsigned long long)st_sec_done);
+        atomicAdd(a.stats + kStatSecWaitPri, (unsigned long long)st_sec_waitpri);
+        atomicAdd(a.stats + kStatDoneTrips, (unsigned long long)st_done_trips);
+        atomicAdd(a.stats + kStatDoneLaneTrips, (unsigned long long)st_done_lanes);
     }
 }
 
