@@ -229,6 +229,10 @@ typedef struct rt_trace_info {
     uint32_t OrderedLaunches; /* heaviest-first re-sorts done for this key   */
     uint32_t ClusteredWalk;   /* 1: secondary rays used the cluster walk     */
     uint32_t GroupsPerRuleSet;/* sphere groups of the rule set traced        */
+    uint32_t SplitHeadFrames; /* > 0: a key's first launch ran as two trace
+                                 launches, these frames first in the cull
+                                 pass's order (measuring tile costs), the rest
+                                 heaviest-first; the same bits as one launch  */
 } rt_trace_info;
 int rt_trace_last_info(rt_device *dev, rt_trace_info *out);
 

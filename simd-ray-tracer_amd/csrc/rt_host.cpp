@@ -52,9 +52,10 @@ struct rt_device {
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
     int tile_sched = 1;
     uint32_t n_sorts = 0;             // re-sorts done for the current tile key
-    int probe_env = 1;                // RT_PROBE=0: no probe launch before the first launch of a key
-    void *d_probe = nullptr;          // probe launch's scratch images + ray counter
-    size_t probe_cap = 0;
+    int split_env = 1;                // RT_PROBE=0: a key's first launch is not split (below)
+    uint32_t head_samples = 8;        // samples per lane of the split's head (RT_HEAD_SAMPLES)
+    uint32_t split_parts = 2;         // launches of a split first launch (RT_SPLIT_PARTS, <= 8)
+    uint32_t split_growth = 3;        // each leading part this many times the previous (RT_SPLIT_GROWTH)
     uint32_t order_launches = 6;      // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept
     uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
     uint32_t *d_tile_live = nullptr;
@@ -144,7 +145,13 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     const char *clu = getenv("RT_CLUSTERS");
     if (clu && (clu[0] == '0' || clu[0] == '2')) d->clusters_env = clu[0] - '0';
     const char *pe = getenv("RT_PROBE");
-    if (pe && pe[0] == '0') d->probe_env = 0;
+    if (pe && pe[0] == '0') d->split_env = 0;
+    const char *hs = getenv("RT_HEAD_SAMPLES");
+    if (hs && atoi(hs) > 0) d->head_samples = (uint32_t)atoi(hs);
+    const char *sp = getenv("RT_SPLIT_PARTS");
+    if (sp && atoi(sp) >= 1 && atoi(sp) <= 8) d->split_parts = (uint32_t)atoi(sp);
+    const char *sgr = getenv("RT_SPLIT_GROWTH");
+    if (sgr && atoi(sgr) >= 1) d->split_growth = (uint32_t)atoi(sgr);
     const char *ol = getenv("RT_ORDER_LAUNCHES");
     if (ol) d->order_launches = (uint32_t)atoi(ol);
     const char *il = getenv("RT_INTERLEAVE");
@@ -186,7 +193,6 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_tile_live);
     (void)hipFree(d->d_cull_counters);
     (void)hipFree(d->d_masks);
-    (void)hipFree(d->d_probe);
     (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
@@ -872,6 +878,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         d->tile_key.clear();
     }
     const bool new_key = key != d->tile_key;
+    uint32_t head_frames = 0;  // > 0: split this launch (first launch of a key, below): frames of the leading parts
+    uint32_t split[8], n_split = 0;
     if (new_key) {
         d->tile_key = key;
         d->n_sorts = 0;
@@ -892,41 +900,25 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
                 d->dead_pixels += c[64 + i];
             }
             d->tile_order_valid = true;
-            // Probe: the first launch of a key has no measured tile costs, and in the
-            // cull pass's live-first order its heavy tiles start late and form the
-            // tail (C2 cold 7.5 ms against 5.4 warm).  A long launch is therefore
-            // preceded by a probe of one sample per lane (P frames, 1/64 of C2's
-            // work) into scratch images that measures the tile costs; the real
-            // launch then runs heaviest-first.  Nothing of the probe is kept but
-            // the order (its images and ray count go to scratch), so every output
-            // bit is unchanged.
-            const bool probe = sched && d->probe_env && d->n_live > 0 && desc->Frames >= 16u * (uint32_t)lpp;
-            if (probe) {
-                const size_t px = (size_t)local_rows * desc->Width;
-                const size_t need = px * 20u + 256u;
-                if (need > d->probe_cap) {
-                    HIP_OK(hipStreamSynchronize(s));
-                    (void)hipFree(d->d_probe);
-                    d->d_probe = nullptr;
-                    d->probe_cap = 0;
-                    if (hipMalloc(&d->d_probe, need) != hipSuccess) return fail(RT_ENOMEM, "rt_trace: probe images");
-                    d->probe_cap = need;
+            // The first launch of a key has no measured tile costs, and in the cull
+            // pass's live-first order its heavy tiles start late and form the tail
+            // (C2 cold 7.7 ms against 5.4 warm).  A long launch is therefore split:
+            // its first head_samples samples per lane (1/8 of C2's work) run in that
+            // order and measure the tile costs, and the remaining frames continue the
+            // running mean heaviest-first.  Splitting a launch at a frame boundary
+            // changes no bit: the owner lane folds frames in order either way, and
+            // frame k's seed and weights depend on PreviousRayCount + k only.
+            const uint32_t split_min = 4u * d->head_samples * (uint32_t)lpp;
+            if (sched && d->split_env && d->n_live > 0 && desc->Frames >= split_min) {
+                // leading parts of head_samples, x split_growth, ... samples per lane
+                // while the rest keeps at least half the frames
+                uint32_t f = d->head_samples * (uint32_t)lpp, used = 0;
+                for (uint32_t i = 0; i + 1 < d->split_parts && used + f <= desc->Frames / 2u; ++i) {
+                    split[n_split++] = f;
+                    used += f;
+                    f *= d->split_growth;
                 }
-                TraceArgs pa = a;
-                pa.prev = (float4 *)d->d_probe;
-                pa.cur = (uint32_t *)((char *)d->d_probe + px * 16u);
-                pa.rays = (unsigned long long *)((char *)d->d_probe + px * 20u);
-                pa.prev_count = 0;
-                pa.frames = (uint32_t)lpp;
-                pa.flags = a.flags | kFlagAccumZero;
-                pa.stats = nullptr;
-                pa.wave_times = nullptr;
-                pa.masks = d->d_masks;
-                pa.tile_order = d->d_tile_order;  // the cull pass's live-first order
-                pa.tile_cost = d->d_tile_cost;
-                if (rtk_launch_trace_grid(&pa, desc->EnableSIMD ? 1 : 0, src, 1, lpp, d->n_live, s) != 0 ||
-                    rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
-                    return fail(RT_EIO, "rt_trace: probe launch failed: %s", hipGetErrorString(hipGetLastError()));
+                head_frames = used;
             }
         } else {
             HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_tiles * 4u, s));
@@ -946,21 +938,35 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     d->last.OrderedLaunches = d->n_sorts;
     d->last.ClusteredWalk = a.clusters ? 1u : 0u;
     d->last.GroupsPerRuleSet = a.n_groups;
-    if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
-        return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-    if (empty_capable && d->n_live < n_tiles &&
-        rtk_launch_empty(&a, lpp, d->d_tile_live, (unsigned long long)(d->dead_pixels * desc->Frames), s) != 0)
-        return fail(RT_EIO, "rt_trace: empty-tile launch failed: %s", hipGetErrorString(hipGetLastError()));
-    // the learned order settles within a few launches (C2: 7.7, 6.3, 6.1, 5.9,
-    // 5.8 ms); after order_launches re-sorts (RT_ORDER_LAUNCHES, default 6)
-    // the order is kept and the three sort kernels (~14 us per launch, 1.5 %
-    // of an 8-rank C2 share) are skipped
-    if (sched && d->n_live > 0 && d->n_sorts < d->order_launches) {
-        d->n_sorts += 1;
-        if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
-            return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
-        d->tile_order_valid = true;
+    // one launch, or the split of a key's first launch (above): the leading
+    // parts, then the rest, each continuing the running mean heaviest-first
+    split[n_split++] = desc->Frames - head_frames;
+    uint32_t done_frames = 0;
+    for (uint32_t part = 0; part < n_split; ++part) {
+        if (part > 0) {
+            a.prev_count = desc->PreviousRayCount + done_frames;
+            a.flags &= ~kFlagAccumZero;
+            a.tile_order = d->d_tile_order;
+        }
+        a.frames = split[part];
+        done_frames += split[part];
+        if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
+            return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+        if (empty_capable && d->n_live < n_tiles &&
+            rtk_launch_empty(&a, lpp, d->d_tile_live, (unsigned long long)(d->dead_pixels * a.frames), s) != 0)
+            return fail(RT_EIO, "rt_trace: empty-tile launch failed: %s", hipGetErrorString(hipGetLastError()));
+        // the learned order settles within a few launches (C2: 7.7, 6.3, 6.1, 5.9,
+        // 5.8 ms); after order_launches re-sorts (RT_ORDER_LAUNCHES, default 6)
+        // the order is kept and the three sort kernels (~14 us per launch, 1.5 %
+        // of an 8-rank C2 share) are skipped
+        if (sched && d->n_live > 0 && (d->n_sorts < d->order_launches || part + 1 < n_split)) {
+            d->n_sorts += 1;
+            if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
+                return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
+            d->tile_order_valid = true;
+        }
     }
+    d->last.SplitHeadFrames = head_frames;
     return RT_OK;
 }
 

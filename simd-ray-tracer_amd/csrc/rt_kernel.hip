@@ -896,6 +896,8 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         accz = pv.z;
     }
 
+    // owner lanes of in-image pixels (they fold until every frame is folded)
+    const uint64_t folding = ballot_and(owner, valid);
     // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left
     uint32_t k = j;            // this lane's next (or current) sample
     uint32_t folded = 0;       // owner: samples folded so far
@@ -959,10 +961,12 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
             : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
                      : folded;
-        const bool can_start = mode == 0u && (P == 1 || k < folded_g + kRing);
-        const uint64_t pri = __ballot(can_start);
-        const uint64_t sec = __ballot(mode == 1u);
-        const uint64_t alive = __ballot(mode != 2u || (owner && valid && folded < a.frames));
+        // (lane masks from single compares: see ballot_and)
+        const bool ring_ok = P == 1 || k < folded_g + kRing;
+        const bool can_start = mode == 0u && ring_ok;
+        const uint64_t pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
+        const uint64_t sec = __builtin_amdgcn_ballot_w64(mode == 1u);
+        const uint64_t alive = __builtin_amdgcn_ballot_w64(mode != 2u) | (folding & __builtin_amdgcn_ballot_w64(folded < a.frames));
         if (alive == 0) break;
         const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
         if ((pri | sec) != 0) {
@@ -988,8 +992,10 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                     st_pri_done += __builtin_popcountll(__ballot(mode == 2u));
                 }
             }
-            const bool traces = do_sec ? mode == 1u : can_start;
-            if (a.max_bounce != 0) nrays += __builtin_popcountll(__ballot(traces));
+            // do_sec ? mode == 1 : can_start, as one compare against a uniform mode
+            // and a uniform override of the ring test (no lane-mask select)
+            const bool traces = mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
+            if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
             if (traces) {
                 if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
                 bool done;

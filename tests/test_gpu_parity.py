@@ -517,23 +517,43 @@ def test_scene_above_the_limit_is_refused(rt, torch_cuda, gdev):
         gdev.upload_scene(rt.scene_from_spheres(sp))
 
 
-def test_probe_launch_changes_no_bit(rt, orc, torch_cuda, monkeypatch):
-    """The first launch of a key (frames >= 16 P) is preceded by a probe launch
-    into scratch images that measures tile costs for a heaviest-first order:
-    the frame, the accumulation and the ray count equal those of the launch
-    without it (RT_PROBE=0), and the oracle's."""
+@pytest.mark.parametrize("simd", [True, False], ids=["simd", "scalar"])
+def test_first_launch_split_changes_no_bit(rt, orc, torch_cuda, monkeypatch, simd):
+    """The first launch of a key (frames >= 32 P) runs split: a head of 8 samples
+    per lane in the cull pass's order, which measures the tile costs, then the
+    rest heaviest-first, continuing the running mean (and with RT_SPLIT_PARTS=3
+    a second leading part of 8 per lane).  The frame, the accumulation and the
+    ray count equal the unsplit launch's (RT_PROBE=0) and the oracle's -- also
+    continuing a resident mean (PreviousRayCount > 0) and with
+    RT_FLAG_ACCUM_ZERO over a stale buffer."""
     monkeypatch.setenv("RT_LANES_PER_PIXEL", "4")
     s, o = _scenes(rt, orc, 1, 64)
-    W, H, S, B = 192, 128, 64, 8
+    W, H, S, B = 192, 128, 128, 8
     cam = rt.camera_setup(s, W, H)
-    out = []
-    for probe in ("0", "1"):
-        monkeypatch.setenv("RT_PROBE", probe)
-        dev = rt.Device(0)
-        try:
-            out.append(gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=S, bounces=B))
-        finally:
-            dev.close()
-    assert torch_cuda.equal(out[0][0], out[1][0]) and torch_cuda.equal(out[0][1], out[1][1]) and out[0][2] == out[1][2]
-    r = orc.render(o, orc.camera(o, W, H), W, H, frames=S, max_bounce=B, threads=orc.cpu_threads())
-    assert_same(*out[1], *r)
+    oc = orc.camera(o, W, H)
+    base = orc.render(o, oc, W, H, frames=7, max_bounce=B, threads=orc.cpu_threads())
+    cases = [("plain", 0, None, False), ("continued", 7, base[0], False), ("accum_zero", 7, base[0], True)]
+    for name, pc, prev0, az in cases:
+        out, heads = [], []
+        for probe, parts in (("0", "2"), ("1", "2"), ("1", "3")):
+            monkeypatch.setenv("RT_PROBE", probe)
+            monkeypatch.setenv("RT_SPLIT_PARTS", parts)
+            monkeypatch.setenv("RT_SPLIT_GROWTH", "1")
+            dev = rt.Device(0)
+            try:
+                prev = None if prev0 is None else torch_cuda.from_numpy(prev0.reshape(-1, 4).copy()).cuda()
+                out.append(gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=S, bounces=B, simd=simd,
+                                      prev_count=pc, prev=prev, accum_zero=az))
+                heads.append(dev.last_info()["SplitHeadFrames"])
+            finally:
+                dev.close()
+        assert heads == [0, 32, 64], (name, heads)
+        for g in out[1:]:
+            assert torch_cuda.equal(out[0][0], g[0]) and torch_cuda.equal(out[0][1], g[1]) and out[0][2] == g[2], name
+        if az or pc == 0:
+            r = orc.render(o, oc, W, H, frames=S, max_bounce=B, simd=simd, threads=orc.cpu_threads(),
+                           prev_count=pc)
+        else:
+            r = orc.render(o, oc, W, H, frames=S, max_bounce=B, simd=simd, threads=orc.cpu_threads(),
+                           prev_count=pc, prev=base[0])
+        assert_same(*out[1], *r)
