@@ -1,6 +1,6 @@
 """Diagnostic: per-wave start/end times of one C2 launch -> occupancy over time.
 env: SPP (256), SIM_RANKS (1: whole frame; G: rank 0's bands of a G-GPU split),
-RT_LANES_PER_PIXEL (auto)."""
+RT_LANES_PER_PIXEL (auto), LAUNCHES (8: the learned order settles)."""
 import os
 import sys
 import pathlib
@@ -20,7 +20,7 @@ rows = rt.band_local_rows(H, 8, G, 0)
 prev = torch.zeros((rows * W, 4), dtype=torch.float32, device="cuda")
 cur = torch.zeros(rows * W, dtype=torch.int32, device="cuda")
 rays = torch.zeros(1, dtype=torch.int64, device="cuda")
-for _ in range(2):
+for _ in range(int(os.environ.get("LAUNCHES", "8"))):
     dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
               frames=S, max_bounce=B, accum_zero=True, band_rows=8, band_count=G, band_index=0)
 torch.cuda.synchronize()

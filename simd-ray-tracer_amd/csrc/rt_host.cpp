@@ -47,6 +47,8 @@ struct rt_device {
     int interleave_env = 0;  // RT_INTERLEAVE=1: wave tiles interleaved over the block tile (P >= 2)
     int scene_global_env = 0;  // RT_SCENE_GLOBAL=1: keep the scene in HBM even when the LDS image could hold it
     int tables_global_env = 0;  // RT_TABLES_LDS=0: the rsqrt and fold-weight tables stay out of the LDS image
+    int solo_env = 1;           // RT_SOLO=0: four waves per workgroup sharing an LDS image (TraceArgs.solo)
+    int walk_any_env = 0;       // RT_WALK_ANY=1: the one-wave kernel dispatches the walk at run time (A/B)
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
@@ -160,6 +162,10 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (sg && sg[0] == '1') d->scene_global_env = 1;
     const char *tl = getenv("RT_TABLES_LDS");  // 0: rsqrt + fold tables read through the caches at every size (A/B)
     if (tl && tl[0] == '0') d->tables_global_env = 1;
+    const char *wa = getenv("RT_WALK_ANY");
+    if (wa && wa[0] == '1') d->walk_any_env = 1;
+    const char *so = getenv("RT_SOLO");
+    if (so && (so[0] == '0' || so[0] == '1')) d->solo_env = so[0] - '0';
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
     const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
@@ -822,6 +828,15 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.lut_in_lds = rtk_lut_in_lds(a.n_groups) && tables ? 1u : 0u;
     a.fold_in_lds = rtk_fold_in_lds(a.n_groups) && tables ? 1u : 0u;
     a.scene_in_lds = a.n_groups <= kMaxLdsGroups && !d->scene_global_env ? 1u : 0u;
+    if (d->solo_env && d->src == kSrcSmem) {  // one-wave workgroups keep no LDS image
+        a.solo = 1u;
+        a.lut_in_lds = a.fold_in_lds = a.scene_in_lds = 0u;
+        if (!a.clusters) a.walk = kWalkGroups;
+        else if (a.cl_words == 1u) a.walk = a.pf_relative ? kWalkCl1Rel : kWalkCl1;
+        else if (a.cl_words == 2u) a.walk = a.pf_relative ? kWalkCl2Rel : kWalkCl2;
+        else a.walk = a.pf_relative ? kWalkCl4Rel : kWalkCl4;
+        if (d->walk_any_env) a.walk = kWalkAny;
+    }
     const int src = a.scene_in_lds ? d->src : kSrcSmem;  // a scene in HBM is read through the scalar cache
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;

@@ -27,7 +27,8 @@ enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // padding members: threshold -inf, bits 0 / q = 0xFFFFFFFF.
 constexpr uint32_t kClEntryF4 = 4;
 constexpr uint32_t kClMaxGroups = 128;   // table built up to this many groups
-constexpr uint32_t kClAutoGroups = 128;  // used by default up to this many (rt_host.cpp clusters_env)
+constexpr uint32_t kClAutoGroups = 64;   // used by default up to this many (rt_host.cpp clusters_env; RTWeekend's
+                                         // 121 groups: 7.8k Mrays/s clustered against 9.4k per group)
 
 // HBM layout of an uploaded scene (per rule set):
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
@@ -67,12 +68,19 @@ struct TraceArgs {
     uint32_t fold_in_lds;        // running-mean weight table in the LDS image (else computed: rtk_fold_in_lds)
     uint32_t scene_in_lds;       // groups + materials copied into the LDS image (else read from HBM: GS kernels)
     uint32_t pf_relative;        // prefilter: row 3 holds r^2 and the threshold is per lane (rt_kernel.hip kPfRel)
+    uint32_t solo;               // one wave per workgroup (4 x tiles workgroups of 64 threads; needs no LDS image)
+    uint32_t walk;               // kWalk*: the one-wave kernel specialised for this launch's secondary walk
 };
+// Secondary-ray walk variants (rt_kernel.hip Walk<>): any (run-time dispatch),
+// the per-group loops, or a cluster walk with 1/2/4 pair-mask words and
+// scene-wide or per-lane ("Rel") thresholds
+enum { kWalkAny = 0, kWalkGroups, kWalkCl1, kWalkCl2, kWalkCl4, kWalkCl1Rel, kWalkCl2Rel, kWalkCl4Rel };
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
        kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatPfRounds, kStatPfGroups,
        kStatPfGroupsNoOwn, kStatPfPairs, kStatPfPairsNoOwn, kStatPfLanePairs, kStatPriBlocked, kStatPriWaitSec,
-       kStatPriDone, kStatSecDone, kStatSecWaitPri, kStatDoneTrips, kStatDoneLaneTrips, kStatCount = 29 };
+       kStatPriDone, kStatSecDone, kStatSecWaitPri, kStatDoneTrips, kStatDoneLaneTrips,
+       kStatSecExact, kStatSecBadLanes, kStatSecZeroDir, kStatCount = 32 };
 constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 
 // Dynamic LDS per block: [rsqrt table] + fold table + groups + materials.

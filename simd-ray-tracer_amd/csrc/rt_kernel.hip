@@ -819,20 +819,42 @@ struct Shape {
 
 // GS: the scene (groups + materials) stays in HBM and per-lane gathers read it
 // through the caches (scenes beyond the LDS image, or RT_SCENE_GLOBAL=1).
-template <bool SIMD, int SRC, bool CULL, int P, bool GS>
-__global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) void trace_kernel(TraceArgs a) {
+// SOLO: one wave per workgroup (block b traces quadrant b & 3 of block tile
+// tile_order[b >> 2]).  A 4-wave workgroup's slots are held until its last wave
+// ends, and a new workgroup needs four free slots at once: at C2 about a fifth
+// of the wave slots sat idle mid-launch (scripts/wave_tail.py).  A one-wave
+// workgroup is replaced as soon as it ends.  It keeps no LDS image (the scene
+// and both tables are read through the caches, measured as fast at C2), only
+// its ring and mask.
+// WALK: the secondary-ray sphere walk compiled into the kernel (rt_kernel.h
+// kWalk*): every variant selected at run time (kWalkAny), the per-group loops
+// only (kWalkGroups), or one cluster walk (pair-mask words, per-lane or
+// scene-wide thresholds).  One walk per kernel keeps the code and the SGPR
+// pressure of the others out of the trace loop (C2 +4 % with only the W = 1
+// walk compiled in).  The exact all-groups loop stays in every variant (rounds
+// whose directions leave the prefilter's |D|^2 bound).
+template <int WALK> struct Walk {
+    static constexpr int W = WALK == kWalkCl2 || WALK == kWalkCl2Rel ? 2 : WALK == kWalkCl4 || WALK == kWalkCl4Rel ? 4 : 1;
+    static constexpr bool REL = WALK == kWalkCl1Rel || WALK == kWalkCl2Rel || WALK == kWalkCl4Rel;
+    static constexpr bool CLUSTERS = WALK >= kWalkCl1;
+};
+
+template <bool SIMD, int SRC, bool CULL, int P, bool GS, bool SOLO = false, int WALK = kWalkAny>
+__global__ __launch_bounds__(SOLO ? 64 : 256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) void trace_kernel(TraceArgs a) {
     static_assert(!GS || SRC == kSrcSmem, "a scene in HBM is read through the scalar cache");
+    static_assert(!SOLO || GS, "a one-wave workgroup keeps no LDS image");
+    constexpr uint32_t kWB = SOLO ? 1u : (uint32_t)kWavesPerBlock;  // waves (LDS slots) per workgroup
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
     constexpr uint32_t kRing = Ring<P>::N;
     extern __shared__ float4 smem[];
     const uint64_t st_entry = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
-    __shared__ uint64_t s_mask[kWavesPerBlock][MaskWords<GS>::N];
+    __shared__ uint64_t s_mask[kWB][MaskWords<GS>::N];
     // ring slot s of pixel pl at s * kRingStride + pl: the sample lanes of a
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
-    __shared__ float4 s_ring[P > 1 ? kWavesPerBlock * kRing * kRingStride : 1];
+    __shared__ float4 s_ring[P > 1 ? kWB * kRing * kRingStride : 1];
     const uint32_t lut_f4 = a.lut_in_lds ? 512u : 0u;  // see rtk_lds_bytes
     const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, a.lut_in_lds != 0u};
     float2 *fold = reinterpret_cast<float2 *>(smem + lut_f4);
@@ -856,16 +878,18 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
             fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
         }
         if (P > 1)
-            for (uint32_t i = threadIdx.x; i < kWavesPerBlock * kRing * kRingStride; i += blockDim.x)
+            for (uint32_t i = threadIdx.x; i < kWB * kRing * kRingStride; i += blockDim.x)
                 s_ring[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    // wave: quadrant of the block tile; sw: the wave's LDS slot in its workgroup
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t wave = SOLO ? blockIdx.x & 3u : tid >> 6, sw = SOLO ? 0u : tid >> 6;
     const uint64_t t_start = a.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
     // Tile of this block: heaviest-first order from the previous launch's
     // measured per-tile cost when the host supplies one (tile_order), so the
     // long tiles do not start last and form the launch's tail.
-    const uint32_t blk = blockIdx.x;
+    const uint32_t blk = SOLO ? blockIdx.x >> 2 : blockIdx.x;
     const uint32_t tile = a.tile_order ? a.tile_order[blk] : blk;
     const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
     const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
@@ -879,11 +903,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     const bool valid = x < a.width && ly < a.local_rows;
     const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
     const bool owner = j == 0;
-    float4 *ring = s_ring + wave * kRing * kRingStride + pl;
+    float4 *ring = s_ring + sw * kRing * kRingStride + pl;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     // the wave tile's primary group mask, from the cull pass (rtk_launch_cull)
-    if (CULL && lane < n_words) s_mask[wave][lane] = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
+    if (CULL && lane < n_words) s_mask[sw][lane] = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
     const uint64_t st_c1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
@@ -907,6 +931,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
     uint32_t st_pri_blocked = 0, st_pri_waitsec = 0, st_pri_done = 0;
     uint32_t st_sec_done = 0, st_sec_waitpri = 0, st_done_trips = 0, st_done_lanes = 0;
+    uint32_t st_sec_exact = 0, st_sec_badlanes = 0, st_sec_zerodir = 0;
     uint64_t st_cyc_pri = 0, st_cyc_sec = 0, st_cyc_fold = 0, st_cyc_setup = 0;
     uint64_t st_cyc_cull = 0, st_cyc_sync = 0, st_cyc_post = 0;
     PfStats st_pf = {0, 0, 0, 0, 0};
@@ -923,7 +948,7 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
     // = RN(Prev*((n-1)/n)) -- folded here without generating the rays.
     bool empty_tile = CULL && !a.use_sky && a.max_bounce != 0;
     if (CULL)
-        for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_mask[wave][w] == 0;
+        for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_mask[sw][w] == 0;
     if (empty_tile) {
         // (an all-zero running mean stays exactly zero: nothing to fold)
         if (valid && owner && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
@@ -1009,9 +1034,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         for (uint32_t w = 0; w < n_words; ++w) {
                             // (readfirstlane returns int: widen each half as u32, or
                             // bit 31 would sign-extend into groups 32..63)
-                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mask[wave][w]);
+                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mask[sw][w]);
                             const uint32_t hi =
-                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[wave][w] >> 32));
+                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[sw][w] >> 32));
                             uint64_t m = (uint64_t)lo | ((uint64_t)hi << 32);
                             if (kStats && a.stats) st_groups += __builtin_popcountll(m);
                             while (m) {
@@ -1025,10 +1050,19 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                         // needs |D|^2 within 2^-16 of 1 on every lane (else exact).
                         const float u2 = __builtin_fmaf(p.rx.y, p.rx.y, __builtin_fmaf(p.ry.y, p.ry.y, p.rz.y * p.rz.y));
                         const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
+                        if (kStats && a.stats && do_sec && !pf) {
+                            st_sec_exact += 1;
+                            st_sec_badlanes += __builtin_popcountll(__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol)));
+                            st_sec_zerodir += __builtin_popcountll(__ballot(u2 == 0.0f));
+                        }
                         if (SRC == kSrcSmem && pf && a.n_cpairs) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             PfStats *ps = kStats && a.stats ? &st_pf : nullptr;
-                            if (a.pf_relative) {
+                            if constexpr (Walk<WALK>::CLUSTERS) {
+                                clustered_groups<SIMD, Walk<WALK>::W, GS, Walk<WALK>::REL>(a, lds_groups, ray, h, ps);
+                            } else if constexpr (WALK == kWalkGroups) {
+                                __builtin_unreachable();  // the host runs kWalkGroups kernels without a cluster table
+                            } else if (a.pf_relative) {
                                 if (a.cl_words == 1u) clustered_groups<SIMD, 1, GS, true>(a, lds_groups, ray, h, ps);
                                 else if (a.cl_words == 2u) clustered_groups<SIMD, 2, GS, true>(a, lds_groups, ray, h, ps);
                                 else clustered_groups<SIMD, 4, GS, true>(a, lds_groups, ray, h, ps);
@@ -1037,11 +1071,11 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
                                 else if (a.cl_words == 2u) clustered_groups<SIMD, 2, GS, false>(a, lds_groups, ray, h, ps);
                                 else clustered_groups<SIMD, 4, GS, false>(a, lds_groups, ray, h, ps);
                             }
-                        } else if (SRC == kSrcSmem && pf && a.pf_relative) {
+                        } else if (SRC == kSrcSmem && pf && a.pf_relative && !Walk<WALK>::CLUSTERS) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             all_groups_smem<SIMD, true, GS, true>(a, lds_groups, ray, h, nullptr, p.own,
                                                                   kStats && a.stats ? &st_pf : nullptr);
-                        } else if (SRC == kSrcSmem && pf) {
+                        } else if (SRC == kSrcSmem && pf && !Walk<WALK>::CLUSTERS) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             all_groups_smem<SIMD, true, GS>(a, lds_groups, ray, h, nullptr, p.own,
                                                         kStats && a.stats ? &st_pf : nullptr);
@@ -1212,6 +1246,9 @@ __global__ __launch_bounds__(256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) 
         atomicAdd(a.stats + kStatSecWaitPri, (unsigned long long)st_sec_waitpri);
         atomicAdd(a.stats + kStatDoneTrips, (unsigned long long)st_done_trips);
         atomicAdd(a.stats + kStatDoneLaneTrips, (unsigned long long)st_done_lanes);
+        atomicAdd(a.stats + kStatSecExact, (unsigned long long)st_sec_exact);
+        atomicAdd(a.stats + kStatSecBadLanes, (unsigned long long)st_sec_badlanes);
+        atomicAdd(a.stats + kStatSecZeroDir, (unsigned long long)st_sec_zerodir);
     }
 }
 
@@ -1523,6 +1560,37 @@ static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n
     const dim3 block(256), grid(n_blocks);
     const size_t lds = rtk_lds_bytes(a);
 #define RTK_LAUNCH(S, R, C, G) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P, G>), grid, block, lds, stream, *a)
+#define RTK_LAUNCH_SOLO(S, C, K) \
+    hipLaunchKernelGGL((rtk::trace_kernel<S, kSrcSmem, C, P, true, true, K>), dim3(4u * n_blocks), dim3(64), 0, stream, *a)
+    if (a->solo) {  // one wave per workgroup, no LDS image (the host clears the *_in_lds flags)
+        // one walk per kernel for the culled production shapes; others dispatch at run time
+        if constexpr (P == 4 || P == 8 || P == 16) {
+            if (cull) {
+#define RTK_WALKS(S)                                                          \
+    switch (a->walk) {                                                        \
+        case kWalkGroups: RTK_LAUNCH_SOLO(S, true, kWalkGroups); return;      \
+        case kWalkCl1: RTK_LAUNCH_SOLO(S, true, kWalkCl1); return;            \
+        case kWalkCl2: RTK_LAUNCH_SOLO(S, true, kWalkCl2); return;            \
+        case kWalkCl4: RTK_LAUNCH_SOLO(S, true, kWalkCl4); return;            \
+        case kWalkCl1Rel: RTK_LAUNCH_SOLO(S, true, kWalkCl1Rel); return;      \
+        case kWalkCl2Rel: RTK_LAUNCH_SOLO(S, true, kWalkCl2Rel); return;      \
+        case kWalkCl4Rel: RTK_LAUNCH_SOLO(S, true, kWalkCl4Rel); return;      \
+        default: break;                                                       \
+    }
+                if (simd) { RTK_WALKS(true) } else { RTK_WALKS(false) }
+#undef RTK_WALKS
+            }
+        }
+        const int key = (simd ? 2 : 0) | (cull ? 1 : 0);
+        switch (key) {
+            case 0: RTK_LAUNCH_SOLO(false, false, kWalkAny); break;
+            case 1: RTK_LAUNCH_SOLO(false, true, kWalkAny); break;
+            case 2: RTK_LAUNCH_SOLO(true, false, kWalkAny); break;
+            default: RTK_LAUNCH_SOLO(true, true, kWalkAny); break;
+        }
+        return;
+    }
+#undef RTK_LAUNCH_SOLO
     if (!a->scene_in_lds) {  // the scene in HBM (the host picks the SMEM source for it)
         const int key = (simd ? 2 : 0) | (cull ? 1 : 0);
         switch (key) {

@@ -225,13 +225,18 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
 
 
 # Kernel variants selected at device creation (rt_host.cpp reads the env):
-# prefilter forced on/off, brute-force primaries, 1/2/32 lanes per pixel, the
-# LDS-staged sphere source.  Every variant must give the same bits as the oracle.
+# prefilter forced on/off, brute-force primaries, 1/2/16/32 lanes per pixel, the
+# LDS-staged sphere source, four-wave workgroups, the run-time walk dispatch.
+# Every variant must give the same bits as the oracle.
 VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"},
                 {"RT_INTERLEAVE": "1"}, {"RT_CULL": "0"}, {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"},
                 {"RT_LANES_PER_PIXEL": "32"}, {"RT_SEC_THRESHOLD": "1"}, {"RT_SPHERE_SRC": "lds"},
                 {"RT_SPHERE_SRC": "lds", "RT_CULL": "0"}, {"RT_SPHERE_SRC": "lds", "RT_CLUSTERS": "0"},
-                {"RT_SCENE_GLOBAL": "1"}, {"RT_SCENE_GLOBAL": "1", "RT_CULL": "0"}]
+                {"RT_SCENE_GLOBAL": "1"}, {"RT_SCENE_GLOBAL": "1", "RT_CULL": "0"},
+                # four-wave workgroups with the LDS image (the default is one wave per
+                # workgroup, each kernel compiled for one secondary walk)
+                {"RT_SOLO": "0"}, {"RT_SOLO": "0", "RT_CLUSTERS": "2"}, {"RT_WALK_ANY": "1"},
+                {"RT_WALK_ANY": "1", "RT_CLUSTERS": "2"}, {"RT_LANES_PER_PIXEL": "16", "RT_CLUSTERS": "2"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
