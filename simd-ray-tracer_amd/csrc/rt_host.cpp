@@ -547,16 +547,13 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
                         m[4 + w] = sphere_xyz(s, kRowZ);
                         m[6 + w] = sphere_r2p(s);
                         m[12 + w] = beta_of_slot[s];
-                        if (*words == 1u) {  // the u64 pair bit itself
-                            const uint64_t bit = 1ull << (s >> 1);
-                            put_u(mb + 8u + 2u * w, (uint32_t)bit);
-                            put_u(mb + 9u + 2u * w, (uint32_t)(bit >> 32));
-                        } else {
-                            put_u(mb + 8u + w, s >> 1);
-                        }
+                        // the u64 bit of pair q = s >> 1 in word q >> 6 of the pair mask
+                        const uint64_t bit = 1ull << ((s >> 1) & 63u);
+                        put_u(mb + 8u + 2u * w, (uint32_t)bit);
+                        put_u(mb + 9u + 2u * w, (uint32_t)(bit >> 32));
+                        put_u(mb + 14u + w, (s >> 1) >> 6);
                     } else {
-                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
-                        if (*words != 1u) put_u(mb + 8u + w, 0xFFFFFFFFu);
+                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit (word 0)
                     }
                 }
             }

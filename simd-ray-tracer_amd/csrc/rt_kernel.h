@@ -14,17 +14,17 @@ enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
 // kClEntryF4 float4 rows, read through the scalar cache --
 //   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1} {b0 b1 0 0}
-//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bits}                      {b0 b1 0 0}
+//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bits0 lo/hi, bits1 lo/hi}  {b0 b1 word0 word1}
 // (b = behind threshold: a lane whose prefilter T = (centre - O).D is below
 // it cannot accept any member -- rt_host.cpp cluster_table)
 // (first/count index member-pair entries; a member's pair q = sphere slot >> 1
 // is its sphere pair in group order, the bit it sets in the wave's pair mask).
-// The wave mask is kept in SGPRs, cl_words u64 words of it:
-//   1 (n_groups <= 32): bits = {lo, hi of 1 << q for member 0, the same for member 1}
-//   2 (n_groups <= 64), 4 (n_groups <= 128): bits = {q0, q1, 0, 0}
+// The wave mask is kept in SGPRs, cl_words u64 words of it (1: n_groups <= 32,
+// 2: <= 64, 4: <= 128): member k's pair q sets bit q & 63 (bits_k = 1 << (q & 63))
+// of word q >> 6 (word_k).
 // With pf_relative the thresholds are per lane: rc2p / r2p hold R_c / r^2 and
 // b the M-free behind bases (rt_host.cpp cluster_table, "relative").
-// padding members: threshold -inf, bits 0 / q = 0xFFFFFFFF.
+// padding members: threshold -inf, bits 0, word 0.
 constexpr uint32_t kClEntryF4 = 4;
 constexpr uint32_t kClMaxGroups = 128;   // table built up to this many groups
 constexpr uint32_t kClAutoGroups = 64;   // used by default up to this many (rt_host.cpp clusters_env; RTWeekend's

@@ -589,13 +589,6 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
 constexpr int kClWords = 4;  // pair-mask words (n_groups <= 128)
-template <int W>
-__device__ __forceinline__ void set_pair(uint64_t (&wave)[kClWords], bool any, uint32_t q) {  // W >= 2: pair index q
-    const uint64_t bit = any ? 1ull << (q & 63u) : 0ull;  // padding (q = ~0) never has any
-#pragma unroll
-    for (int w = 0; w < W; ++w) wave[w] |= (q >> 6) == (uint32_t)w ? bit : 0ull;
-}
-
 // Per-lane thresholds (pf_relative, rt_host.cpp cluster_table "relative"):
 // cluster: e_c >= RN(cc kClRel + R_c); sphere: e >= RN(cc kPfRel + r^2) (kPfRel
 // below); behind: T < RN(b - cc kBehindRel).
@@ -609,12 +602,25 @@ __device__ __forceinline__ uint64_t ballot_and(bool a, bool b) {
     return __builtin_amdgcn_ballot_w64(a) & __builtin_amdgcn_ballot_w64(b);
 }
 
+// Entry e of the cluster table at byte offset off (a 32-bit offset from the
+// table's base keeps the per-entry address arithmetic to one SALU add).
+__device__ __forceinline__ cv4f_t *cl_entry(cv4f_t *ct, uint32_t off) {
+    return (cv4f_t *)((const __attribute__((address_space(4))) char *)ct + off);
+}
+constexpr uint32_t kClEntryBytes = 16u * kClEntryF4;
+
+// The member pairs [first, first + count) of an entered cluster: a sphere pair
+// some lane may hit ORs its pair bit into word `word` of the wave's pair mask
+// (r2 = the u64 bits of member 0 and 1, r3.zw = their words).  The walk is
+// SALU-heavy (ballots, mask merges, loop control issue on the CU's one scalar
+// unit): C5's member loop at 48 SALU per entry ran 17 % slower than at 34.
 template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
                                              uint64_t (&wave)[kClWords], PfStats *ps) {
     if (ps) ps->groups += count;
-    for (uint32_t m = first; m < first + count; ++m) {
-        cv4f_t *e = ct + kClEntryF4 * m;
+    const uint32_t end = (first + count) * kClEntryBytes;
+    for (uint32_t off = first * kClEntryBytes; off != end; off += kClEntryBytes) {
+        cv4f_t *e = cl_entry(ct, off);
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];
         f2 T, cc;
@@ -626,13 +632,15 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
         const bool f0 = ballot_and(!(v.x >= t0), !(T.x < b0)) != 0;
         const bool f1 = ballot_and(!(v.y >= t1), !(T.y < b1)) != 0;
-        if (W == 1) {  // precomputed pair bits
-            const uint64_t b0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
-            const uint64_t b1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
-            wave[0] |= (f0 ? b0 : 0ull) | (f1 ? b1 : 0ull);
+        const uint64_t bits0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
+        const uint64_t bits1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
+        const uint64_t m0 = f0 ? bits0 : 0ull, m1 = f1 ? bits1 : 0ull;
+        if (W == 1) {
+            wave[0] |= m0 | m1;
         } else {
-            set_pair<W>(wave, f0, __float_as_uint(r2.x));
-            set_pair<W>(wave, f1, __float_as_uint(r2.y));
+            const uint32_t w0 = __float_as_uint(r3.z), w1 = __float_as_uint(r3.w);
+#pragma unroll
+            for (int w = 0; w < W; ++w) wave[w] |= (w0 == (uint32_t)w ? m0 : 0ull) | (w1 == (uint32_t)w ? m1 : 0ull);
         }
     }
 }
@@ -644,8 +652,8 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
                                                  Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
-    for (uint32_t c = 0; c < a.n_cpairs; ++c) {
-        cv4f_t *e = ct + kClEntryF4 * c;
+    for (uint32_t off = 0, end = a.n_cpairs * kClEntryBytes; off != end; off += kClEntryBytes) {
+        cv4f_t *e = cl_entry(ct, off);
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];
         f2 T, cc;

@@ -218,16 +218,14 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
             for m in range(first, first + count):
                 e = tab[m]
                 words = e[2].view(np.uint32)
-                one_word = len(r2) // 4 <= 32  # kernel's cl_words == 1: u64 pair bits, else pair indices
-                pair = [int(words[2 * w]) | (int(words[2 * w + 1]) << 32) for w in range(2)] if one_word else \
-                    [int(words[w]) for w in range(2)]
+                word_of = e[3].view(np.uint32)[2:4]  # member k's pair q: bit q & 63 of mask word q >> 6
+                pair = [int(words[2 * w]) | (int(words[2 * w + 1]) << 32) for w in range(2)]
                 for w in range(2):
                     if np.isneginf(e[1][2 + w]):
-                        assert pair[w] == (0 if one_word else 0xFFFFFFFF)
+                        assert pair[w] == 0 and word_of[w] == 0
                         continue
-                    if one_word:
-                        assert pair[w] and pair[w] & (pair[w] - 1) == 0, "one pair bit per member"
-                        pair[w] = pair[w].bit_length() - 1
+                    assert pair[w] and pair[w] & (pair[w] - 1) == 0, "one pair bit per member"
+                    pair[w] = pair[w].bit_length() - 1 + 64 * int(word_of[w])
                     x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
                     s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
                                        (r2p == t) & live)
