@@ -401,7 +401,9 @@ def main():
         workload = (f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
                     + ("" if args.scene == 1 else f", {SCENE_NAMES[args.scene]}") + view)
         pmc = pmc_record(workload)
-        kernel = f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{info['LanesPerPixel']}>"
+        walks = {0: "any", 1: "groups", 2: "cl1", 3: "cl2", 4: "cl4", 5: "cl1rel", 6: "cl2rel", 7: "cl4rel"}
+        kernel = (f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{info['LanesPerPixel']},"
+                  f"{'one-wave' if info['OneWaveGroups'] else 'four-wave'},walk={walks.get(info['Walk'], '?')}>")
         roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1), "unit": "TFLOP/s",
                 "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": round(kern_ms, 3)}
         if pmc:

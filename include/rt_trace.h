@@ -233,6 +233,11 @@ typedef struct rt_trace_info {
                                  launches, these frames first in the cull
                                  pass's order (measuring tile costs), the rest
                                  heaviest-first; the same bits as one launch  */
+    uint32_t OneWaveGroups;   /* 1: one wave per workgroup (no LDS image)    */
+    uint32_t Walk;            /* secondary walk compiled into the kernel: 0
+                                 run-time dispatch, 1 per-group loops, 2/3/4
+                                 cluster walk with 1/2/4 mask words, 5/6/7
+                                 the same with per-lane thresholds           */
 } rt_trace_info;
 int rt_trace_last_info(rt_device *dev, rt_trace_info *out);
 

@@ -950,6 +950,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     d->last.OrderedLaunches = d->n_sorts;
     d->last.ClusteredWalk = a.clusters ? 1u : 0u;
     d->last.GroupsPerRuleSet = a.n_groups;
+    d->last.OneWaveGroups = a.solo;
+    d->last.Walk = a.walk;
     // one launch, or the split of a key's first launch (above): the leading
     // parts, then the rest, each continuing the running mean heaviest-first
     split[n_split++] = desc->Frames - head_frames;
