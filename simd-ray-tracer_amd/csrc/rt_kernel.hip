@@ -89,12 +89,12 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 }
 
 // RN(a/b) from y = RN(1/b) (Markstein: q0 = a*y, exact residual, one fma
-// correction) for b > 0 and a == +-0 or |a/b| >= 2^-100 (no underflow in
-// the residual); the sign bit of a is copied so -0/b stays -0.
+// correction) for b > 0 and a == +0 or |a/b| >= 2^-100 (no underflow in the
+// residual).  a == -0 would come out +0: neither caller divides one (the film
+// numerator is never -0; normalize sends any zero quotient to its IEEE path).
 __device__ __forceinline__ float div_rn(float a, float b, float y) {
     const float q0 = a * y;
-    const float q = __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
-    return __uint_as_float((__float_as_uint(q) & 0x7FFFFFFFu) | (__float_as_uint(a) & 0x80000000u));
+    return __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
 }
 
 // v3::Normalize (x64_math.h:234-245): IEEE divide by the correctly rounded
@@ -216,7 +216,8 @@ __device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t
     const float jx = rand_float(p.rng, -0.5f, kInvRange1);
     const float jy = rand_float(p.rng, -0.5f, kInvRange1);
     // ((x + Jx) * 2) / W with W's reciprocal RN(1/W) from the host: the
-    // numerator is 0 or >= 2^-24, so div_rn's range condition holds
+    // numerator is +0 or >= 2^-24 (Jx = -0.5 + r is never -0), so div_rn's
+    // range condition holds
     const float fx = -1.0f + div_rn(((float)x + jx) * 2.0f, (float)a.width, a.inv_width);
     const float fy = -1.0f + div_rn(((float)y + jy) * 2.0f, (float)a.height, a.inv_height);
     const float kx = (fx * a.film_w) * 0.5f;
@@ -805,6 +806,9 @@ struct Ring {
     static constexpr uint32_t N = P <= 4 ? 8u : 2u * (uint32_t)P;
 };
 
+#ifndef RTK_SOLO_WAVES_PER_SIMD  // the same target for the one-wave kernels (A/B: make variant KFLAGS=-DRTK_SOLO_WAVES_PER_SIMD=8)
+#define RTK_SOLO_WAVES_PER_SIMD 7
+#endif
 #ifndef RTK_MIN_WAVES_PER_SIMD  // occupancy target (VGPR budget) of the production (SMEM) kernels;
 #define RTK_MIN_WAVES_PER_SIMD 7   // 7 waves = 72 VGPRs, no VGPR spills: measured best on C2 with the
 #endif                             // cluster walk (w6 116.5k, w7 120.0-121.1k, w8 118.2k Mrays/s, w8 spills)
@@ -848,7 +852,8 @@ template <int WALK> struct Walk {
 };
 
 template <bool SIMD, int SRC, bool CULL, int P, bool GS, bool SOLO = false, int WALK = kWalkAny>
-__global__ __launch_bounds__(SOLO ? 64 : 256, SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1) void trace_kernel(TraceArgs a) {
+__global__ __launch_bounds__(SOLO ? 64 : 256, SOLO ? RTK_SOLO_WAVES_PER_SIMD : SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1)
+void trace_kernel(TraceArgs a) {
     static_assert(!GS || SRC == kSrcSmem, "a scene in HBM is read through the scalar cache");
     static_assert(!SOLO || GS, "a one-wave workgroup keeps no LDS image");
     constexpr uint32_t kWB = SOLO ? 1u : (uint32_t)kWavesPerBlock;  // waves (LDS slots) per workgroup
