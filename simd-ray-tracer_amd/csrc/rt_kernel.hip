@@ -990,6 +990,23 @@ void trace_kernel(TraceArgs a) {
         st_cyc_sync = st_c2 - st_c1;
         st_cyc_post = t - st_c2;
     }
+    // Re-derive the winner's HitNormal / NextRayOrigin exactly as they were
+    // formed at acceptance (main.cpp:423-429), then shade and bounce.
+    auto shade_hit = [&](float tmin, uint32_t sidx, bool inside) {
+        const float *gsph = sph_src + 4u * kGroupF4 * (sidx >> 2) + (sidx & 3u);
+        const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
+        const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
+        const float ipx = p.rx.y * tmin, ipy = p.ry.y * tmin, ipz = p.rz.y * tmin;
+        const float hx = ipx - cx, hy = ipy - cy, hz = ipz - cz;
+        p.rx.x = p.rx.x + ipx;
+        p.ry.x = p.ry.x + ipy;
+        p.rz.x = p.rz.x + ipz;
+        const float4 cs = mat_src[2u * sidx + 0u];
+        const float4 ei = mat_src[2u * sidx + 1u];
+        shade(lut, cs, ei, hx, hy, hz, inside, p);
+        if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
+        p.bounce += 1;
+    };
     for (;;) {
         // ring space: sample k may start once k < folded + kRing (the oldest
         // unfolded sample's lane is never blocked, so this cannot deadlock)
@@ -1133,21 +1150,7 @@ void trace_kernel(TraceArgs a) {
                         }
                         done = true;
                     } else {
-                        // Re-derive the winner's HitNormal / NextRayOrigin exactly as
-                        // they were formed at acceptance (main.cpp:423-429).
-                        const float *gsph = sph_src + 4u * kGroupF4 * (sidx >> 2) + (sidx & 3u);
-                        const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
-                        const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
-                        const float ipx = p.rx.y * tmin, ipy = p.ry.y * tmin, ipz = p.rz.y * tmin;
-                        const float hx = ipx - cx, hy = ipy - cy, hz = ipz - cz;
-                        p.rx.x = p.rx.x + ipx;
-                        p.ry.x = p.ry.x + ipy;
-                        p.rz.x = p.rz.x + ipz;
-                        const float4 cs = mat_src[2u * sidx + 0u];
-                        const float4 ei = mat_src[2u * sidx + 1u];
-                        shade(lut, cs, ei, hx, hy, hz, inside, p);
-                        if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
-                        p.bounce += 1;
+                        shade_hit(tmin, sidx, inside);
                         done = p.bounce == a.max_bounce;
                     }
                 }
