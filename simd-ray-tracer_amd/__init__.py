@@ -277,8 +277,10 @@ def scene_prefilter(scene: RtScene, simd: bool = True):
 
 
 def scene_clusters(scene: RtScene, simd: bool = True):
-    """The clustered prefilter table rt_scene_upload builds: (table (n, 4, 4)
-    f32 rows, n_cpairs); n_cpairs == 0 means the per-group loop is used."""
+    """The clustered prefilter table rt_scene_upload builds: (table (n, rows, 4)
+    f32, n_cpairs) with rows = 4 for a one-word pair mask (<= 32 groups), else
+    3 + words (rt_kernel.h cl_entry_f4); n_cpairs == 0 means the per-group loop
+    is used."""
     nf4, ncp = c_uint32(), c_uint32()
     _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), None, 0, ctypes.byref(nf4), ctypes.byref(ncp)),
            "rt_scene_clusters")
@@ -286,7 +288,9 @@ def scene_clusters(scene: RtScene, simd: bool = True):
     if nf4.value:
         _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), tab.ctypes.data, nf4.value, ctypes.byref(nf4),
                                        ctypes.byref(ncp)), "rt_scene_clusters")
-    return tab.reshape(-1, 4, 4), int(ncp.value)
+    groups = (scene.ScalarSpheres.Count + 3) // 4
+    words = 1 if groups <= 32 else 2 if groups <= 64 else 4
+    return tab.reshape(-1, 4 if words == 1 else 3 + words, 4), int(ncp.value)
 
 
 def rsqrt_table_builtin() -> np.ndarray:

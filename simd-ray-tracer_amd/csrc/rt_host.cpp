@@ -301,7 +301,7 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
     return n_ratio > 0 && ratio / n_ratio < 0.5;
 }
 
-// Clustered prefilter table (rt_kernel.h, kClEntryF4 rows per entry) for the
+// Clustered prefilter table (rt_kernel.h, cl_entry_f4(words) rows per entry) for the
 // secondary-ray sphere loop: the hittable spheres are grouped into about
 // sqrt(n) spatial clusters (deterministic k-means; any membership -- the
 // exact test still runs in the reference's group order).  A cluster c with
@@ -514,7 +514,8 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     const uint32_t n_cp = (uint32_t)cl.size() / 2u;
     uint32_t n_mp = 0;
     for (const Cl &C : cl) n_mp += ((uint32_t)C.mem.size() + 1u) / 2u;
-    tab.assign((size_t)(n_cp + n_mp) * kClEntryF4 * 4u, 0.0f);
+    const uint32_t ef = cl_entry_f4(*words) * 4u;  // floats per entry
+    tab.assign((size_t)(n_cp + n_mp) * ef, 0.0f);
     auto put_u = [&](size_t at, uint32_t v) { memcpy(&tab[at], &v, 4); };
     auto sphere_xyz = [&](uint32_t s, int axis) {
         const uint32_t g = (s / 4u) * 4u * kGroupF4, l = s % 4u;
@@ -526,18 +527,18 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     };
     uint32_t next = n_cp;
     for (uint32_t p = 0; p < n_cp; ++p) {
-        float *e = &tab[(size_t)p * kClEntryF4 * 4u];
+        float *e = &tab[(size_t)p * ef];
         const Cl &A = cl[2u * p], &B = cl[2u * p + 1u];
         e[0] = A.qx, e[1] = B.qx, e[2] = A.qy, e[3] = B.qy, e[4] = A.qz, e[5] = B.qz, e[6] = A.t, e[7] = B.t;
         e[12] = A.b, e[13] = B.b;
         const Cl *two[2] = {&A, &B};
         for (int h = 0; h < 2; ++h) {
             const uint32_t cnt = ((uint32_t)two[h]->mem.size() + 1u) / 2u;
-            put_u((size_t)p * kClEntryF4 * 4u + 8u + 2u * h, next);
-            put_u((size_t)p * kClEntryF4 * 4u + 9u + 2u * h, cnt);
+            put_u((size_t)p * ef + 8u + 2u * h, next);
+            put_u((size_t)p * ef + 9u + 2u * h, cnt);
             for (uint32_t q = 0; q < cnt; ++q, ++next) {
-                float *m = &tab[(size_t)next * kClEntryF4 * 4u];
-                const size_t mb = (size_t)next * kClEntryF4 * 4u;
+                float *m = &tab[(size_t)next * ef];
+                const size_t mb = (size_t)next * ef;
                 for (int w = 0; w < 2; ++w) {
                     const uint32_t idx = 2u * q + (uint32_t)w;
                     if (idx < two[h]->mem.size()) {
@@ -547,13 +548,15 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
                         m[4 + w] = sphere_xyz(s, kRowZ);
                         m[6 + w] = sphere_r2p(s);
                         m[12 + w] = beta_of_slot[s];
-                        // the u64 bit of pair q = s >> 1 in word q >> 6 of the pair mask
+                        // the u64 bit of pair q = s >> 1 in the row of word q >> 6 (row 2
+                        // for word 0, row 3 + w for word w >= 1; the other words' rows stay 0)
                         const uint64_t bit = 1ull << ((s >> 1) & 63u);
-                        put_u(mb + 8u + 2u * w, (uint32_t)bit);
-                        put_u(mb + 9u + 2u * w, (uint32_t)(bit >> 32));
-                        put_u(mb + 14u + w, (s >> 1) >> 6);
+                        const uint32_t word = (s >> 1) >> 6;
+                        const size_t row = word == 0u ? 8u : 4u * (3u + word);
+                        put_u(mb + row + 2u * w, (uint32_t)bit);
+                        put_u(mb + row + 1u + 2u * w, (uint32_t)(bit >> 32));
                     } else {
-                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit (word 0)
+                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
                     }
                 }
             }

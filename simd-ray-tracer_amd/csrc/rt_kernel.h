@@ -12,20 +12,22 @@ constexpr uint32_t kRowR2P = 3;       //   prefilter thresholds (rows 0-3 = one 
 constexpr uint32_t kRowR2 = 4;        //   r*r
 enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
-// kClEntryF4 float4 rows, read through the scalar cache --
-//   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1} {b0 b1 0 0}
-//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {bits0 lo/hi, bits1 lo/hi}  {b0 b1 word0 word1}
+// cl_entry_f4(W) float4 rows, read through the scalar cache --
+//   cluster pair c : {qx0 qx1 qy0 qy1} {qz0 qz1 rc2p0 rc2p1} {first0 count0 first1 count1} {b0 b1 0 0} [padding]
+//   member pair m  : {x0 x1 y0 y1}     {z0 z1 r2p0 r2p1}     {word-0 bits of member 0 (lo, hi), of member 1}
+//                    {b0 b1 0 0}  then one row per further word w = 1 .. W-1: {word-w bits of member 0, of member 1}
 // (b = behind threshold: a lane whose prefilter T = (centre - O).D is below
 // it cannot accept any member -- rt_host.cpp cluster_table)
 // (first/count index member-pair entries; a member's pair q = sphere slot >> 1
 // is its sphere pair in group order, the bit it sets in the wave's pair mask).
-// The wave mask is kept in SGPRs, cl_words u64 words of it (1: n_groups <= 32,
-// 2: <= 64, 4: <= 128): member k's pair q sets bit q & 63 (bits_k = 1 << (q & 63))
-// of word q >> 6 (word_k).
+// The wave mask is kept in SGPRs, W = cl_words u64 words of it (1: n_groups <= 32,
+// 2: <= 64, 4: <= 128): member k's pair q sets bit q & 63 of word q >> 6, and its
+// entry holds that bit in the row of word q >> 6 and 0 in the others, so the kernel
+// merges a flagged member into every word with one select and one OR each.
 // With pf_relative the thresholds are per lane: rc2p / r2p hold R_c / r^2 and
 // b the M-free behind bases (rt_host.cpp cluster_table, "relative").
-// padding members: threshold -inf, bits 0, word 0.
-constexpr uint32_t kClEntryF4 = 4;
+// padding members: threshold -inf, bits 0.
+constexpr uint32_t cl_entry_f4(uint32_t words) { return words == 1u ? 4u : 3u + words; }
 constexpr uint32_t kClMaxGroups = 128;   // table built up to this many groups
 constexpr uint32_t kClAutoGroups = 128;  // used by default up to this many (rt_host.cpp clusters_env; RTWeekend's
                                          // 121 groups: 11.3k Mrays/s clustered against 9.4k per group)
@@ -60,7 +62,7 @@ struct TraceArgs {
     uint32_t *tile_cost;         // optional: per-tile cost (max wave shader cycles), atomicMax'd
     const uint64_t *masks;       // CULL: per wave tile (4*tile + wave) n_words primary group masks
     uint32_t tiles_x;            // block tiles per row (2TW x 2TH pixels each)
-    const float4 *clusters;      // optional: clustered prefilter table (kClEntryF4 rows per entry)
+    const float4 *clusters;      // optional: clustered prefilter table (cl_entry_f4(cl_words) rows per entry)
     uint32_t n_cpairs;           // cluster-pair entries at its start; 0 = per-group prefilter loop
     uint32_t cl_words;           // u64 words of the clustered loop's pair mask (1 or 2)
     uint32_t interleave;         // wave tiles interleave over the block tile (P >= 2 only)

@@ -608,19 +608,53 @@ __device__ __forceinline__ uint64_t ballot_and(bool a, bool b) {
 __device__ __forceinline__ cv4f_t *cl_entry(cv4f_t *ct, uint32_t off) {
     return (cv4f_t *)((const __attribute__((address_space(4))) char *)ct + off);
 }
-constexpr uint32_t kClEntryBytes = 16u * kClEntryF4;
 
 // The member pairs [first, first + count) of an entered cluster: a sphere pair
-// some lane may hit ORs its pair bit into word `word` of the wave's pair mask
-// (r2 = the u64 bits of member 0 and 1, r3.zw = their words).  The walk is
+// some lane may hit ORs its word-w bits into every word w of the wave's pair
+// mask (rt_kernel.h: the entry's row of word w holds the bit or 0).  The walk is
 // SALU-heavy (ballots, mask merges, loop control issue on the CU's one scalar
 // unit): C5's member loop at 48 SALU per entry ran 17 % slower than at 34.
+// wave[w] |= f ? bits[w] : 0 for every word under one compare of the ballot f:
+// s_cselect_b64 per word (the compiler's lowering selects 32-bit halves, two
+// per word) -- the merge runs on the CU's one scalar unit for every member.
+template <int W>
+__device__ __forceinline__ void merge_words(uint64_t (&wave)[kClWords], uint64_t f, const uint64_t (&bits)[W]) {
+    uint64_t t0, t1;
+    if constexpr (W == 2) {
+        asm("s_cmp_lg_u64 %[f], 0\n\t"
+            "s_cselect_b64 %[t0], %[b0], 0\n\t"
+            "s_cselect_b64 %[t1], %[b1], 0\n\t"
+            "s_or_b64 %[w0], %[w0], %[t0]\n\t"
+            "s_or_b64 %[w1], %[w1], %[t1]"
+            : [w0] "+s"(wave[0]), [w1] "+s"(wave[1]), [t0] "=&s"(t0), [t1] "=&s"(t1)
+            : [f] "s"(f), [b0] "s"(bits[0]), [b1] "s"(bits[1])
+            : "scc");
+    } else {
+        static_assert(W == 4, "pair-mask words");
+        uint64_t t2, t3;
+        asm("s_cmp_lg_u64 %[f], 0\n\t"
+            "s_cselect_b64 %[t0], %[b0], 0\n\t"
+            "s_cselect_b64 %[t1], %[b1], 0\n\t"
+            "s_cselect_b64 %[t2], %[b2], 0\n\t"
+            "s_cselect_b64 %[t3], %[b3], 0\n\t"
+            "s_or_b64 %[w0], %[w0], %[t0]\n\t"
+            "s_or_b64 %[w1], %[w1], %[t1]\n\t"
+            "s_or_b64 %[w2], %[w2], %[t2]\n\t"
+            "s_or_b64 %[w3], %[w3], %[t3]"
+            : [w0] "+s"(wave[0]), [w1] "+s"(wave[1]), [w2] "+s"(wave[2]), [w3] "+s"(wave[3]), [t0] "=&s"(t0),
+              [t1] "=&s"(t1), [t2] "=&s"(t2), [t3] "=&s"(t3)
+            : [f] "s"(f), [b0] "s"(bits[0]), [b1] "s"(bits[1]), [b2] "s"(bits[2]), [b3] "s"(bits[3])
+            : "scc");
+    }
+}
+
 template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
                                              uint64_t (&wave)[kClWords], PfStats *ps) {
+    constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W);
     if (ps) ps->groups += count;
-    const uint32_t end = (first + count) * kClEntryBytes;
-    for (uint32_t off = first * kClEntryBytes; off != end; off += kClEntryBytes) {
+    const uint32_t end = (first + count) * kEntryBytes;
+    for (uint32_t off = first * kEntryBytes; off != end; off += kEntryBytes) {
         cv4f_t *e = cl_entry(ct, off);
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];
@@ -631,17 +665,20 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         const float t1 = REL ? __builtin_fmaf(cc.y, kPfRel, r1.w) : r1.w;
         const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-        const bool f0 = ballot_and(!(v.x >= t0), !(T.x < b0)) != 0;
-        const bool f1 = ballot_and(!(v.y >= t1), !(T.y < b1)) != 0;
-        const uint64_t bits0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
-        const uint64_t bits1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
-        const uint64_t m0 = f0 ? bits0 : 0ull, m1 = f1 ? bits1 : 0ull;
-        if (W == 1) {
-            wave[0] |= m0 | m1;
-        } else {
-            const uint32_t w0 = __float_as_uint(r3.z), w1 = __float_as_uint(r3.w);
+        const uint64_t f0m = ballot_and(!(v.x >= t0), !(T.x < b0)), f1m = ballot_and(!(v.y >= t1), !(T.y < b1));
+        const bool f0 = f0m != 0, f1 = f1m != 0;
+        uint64_t bw0[W], bw1[W];  // member 0 and 1 bits in word w
 #pragma unroll
-            for (int w = 0; w < W; ++w) wave[w] |= (w0 == (uint32_t)w ? m0 : 0ull) | (w1 == (uint32_t)w ? m1 : 0ull);
+        for (int w = 0; w < W; ++w) {
+            const v4f_t rb = w == 0 ? r2 : e[3 + w];
+            bw0[w] = (uint64_t)__float_as_uint(rb.x) | ((uint64_t)__float_as_uint(rb.y) << 32);
+            bw1[w] = (uint64_t)__float_as_uint(rb.z) | ((uint64_t)__float_as_uint(rb.w) << 32);
+        }
+        if constexpr (W == 1) {
+            wave[0] |= (f0 ? bw0[0] : 0ull) | (f1 ? bw1[0] : 0ull);
+        } else {
+            merge_words<W>(wave, f0m, bw0);
+            merge_words<W>(wave, f1m, bw1);
         }
     }
 }
@@ -653,7 +690,8 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
                                                  Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
-    for (uint32_t off = 0, end = a.n_cpairs * kClEntryBytes; off != end; off += kClEntryBytes) {
+    constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W);
+    for (uint32_t off = 0, end = a.n_cpairs * kEntryBytes; off != end; off += kEntryBytes) {
         cv4f_t *e = cl_entry(ct, off);
         const v4f_t r0 = e[0], r1 = e[1];
         const v4f_t r2 = e[2], r3 = e[3];

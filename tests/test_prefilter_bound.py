@@ -217,15 +217,20 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
             ms = []
             for m in range(first, first + count):
                 e = tab[m]
-                words = e[2].view(np.uint32)
-                word_of = e[3].view(np.uint32)[2:4]  # member k's pair q: bit q & 63 of mask word q >> 6
-                pair = [int(words[2 * w]) | (int(words[2 * w + 1]) << 32) for w in range(2)]
+                # member k's pair q: bit q & 63 in the row of mask word q >> 6 (row 2, then rows 4 ..)
+                rows = [e[2]] + [e[3 + w] for w in range(1, max(1, len(e) - 3))]
+                bits = [[int(r.view(np.uint32)[2 * k]) | (int(r.view(np.uint32)[2 * k + 1]) << 32) for r in rows]
+                        for k in range(2)]
+                pair = [0, 0]
                 for w in range(2):
+                    set_words = [i for i, b in enumerate(bits[w]) if b]
                     if np.isneginf(e[1][2 + w]):
-                        assert pair[w] == 0 and word_of[w] == 0
+                        assert not set_words
                         continue
-                    assert pair[w] and pair[w] & (pair[w] - 1) == 0, "one pair bit per member"
-                    pair[w] = pair[w].bit_length() - 1 + 64 * int(word_of[w])
+                    assert len(set_words) == 1, "one mask word per member"
+                    b = bits[w][set_words[0]]
+                    assert b & (b - 1) == 0, "one pair bit per member"
+                    pair[w] = b.bit_length() - 1 + 64 * set_words[0]
                     x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
                     s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
                                        (r2p == t) & live)
