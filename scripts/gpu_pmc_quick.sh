@@ -22,6 +22,6 @@ print(sys.argv[1], "| cycles %.3e" % cyc, "insts_valu %.4e" % c["SQ_INSTS_VALU"]
       "dual %.3f" % (2 * c["SQ_ACTIVE_INST_VALU2"] / c["SQ_ACTIVE_INST_VALU"]), "lanes %.3f" % (c["SQ_THREAD_CYCLES_VALU"] / 64 / c["SQ_ACTIVE_INST_VALU"]),
       "waves %d" % c["SQ_WAVES"], "wavecyc %.3e" % c["SQ_WAVE_CYCLES"], "occ %.2f" % (c["SQ_WAVE_CYCLES"] * 4 / (1024 * cyc)),
       "salu %.3e" % c["SQ_INSTS_SALU"], "waitinst %.3f" % (c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]), "waitany %.3f" % (c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]),
-      "lds %.3e conf %.3e" % (c["SQ_INSTS_LDS"], c["SQ_LDS_BANK_CONFLICT"]))
+      "lds %.3e conf %.3e" % (c["SQ_INSTS_LDS"], c["SQ_LDS_BANK_CONFLICT"]), "smem %.3e" % c["SQ_INSTS_SMEM"], "ms %.3f" % (cyc / 2.4e6))
 PY
 done
