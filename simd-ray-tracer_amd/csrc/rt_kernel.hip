@@ -830,6 +830,10 @@ constexpr bool kStats = false;
 #endif
 
 constexpr int kWavesPerBlock = 4;
+#ifndef RTK_FOLD_BEFORE_PRIMARY  // 1: the owner folds its ring only before primary rounds (A/B)
+#define RTK_FOLD_BEFORE_PRIMARY 1
+#endif
+constexpr bool kFoldBeforePrimary = RTK_FOLD_BEFORE_PRIMARY != 0;
 // primary group mask words per wave tile: the LDS-image kernels keep this
 // small (it is static LDS, and C2's blocks fill the CU's 160 KB 7 times)
 template <bool GS>
@@ -1045,27 +1049,65 @@ void trace_kernel(TraceArgs a) {
         if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
         p.bounce += 1;
     };
+    // the pixel's owner lane's fold cursor (first of its P-lane slice) via DPP
+    auto fold_cursor = [&]() -> uint32_t {
+        return P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
+               : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
+               : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
+                        : folded;
+    };
+    auto fold_ring = [&]() {
+        if (P > 1 && owner && valid) {
+            // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
+            // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
+            // sample's lane.  The fold is one sequential chain per pixel, so the owner
+            // reads kFoldBatch ring slots per LDS round trip (more for more lanes).
+            constexpr uint32_t kFoldBatch = P >= 8 ? 4u : 2u;
+            bool more = true;
+            while (more && folded < a.frames) {
+                float4 r[kFoldBatch];
+#pragma unroll
+                for (uint32_t i = 0; i < kFoldBatch; ++i) r[i] = ring[((folded + i) % kRing) * kRingStride];
+#pragma unroll
+                for (uint32_t i = 0; i < kFoldBatch; ++i) {
+                    more = more && folded < a.frames && __builtin_signbit(r[i].w);
+                    if (more) {
+                        accx = r[i].x + accx * -r[i].w;
+                        accy = r[i].y + accy * -r[i].w;
+                        accz = r[i].z + accz * -r[i].w;
+                        ring[(folded % kRing) * kRingStride].w = 0.0f;
+                        folded += 1u;
+                    }
+                }
+            }
+        }
+    };
     for (;;) {
         // ring space: sample k may start once k < folded + kRing (the oldest
         // unfolded sample's lane is never blocked, so this cannot deadlock)
         // the pixel's owner lane (first of its P-lane quad slice) via DPP
-        const uint32_t folded_g =
-            P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
-            : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
-            : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
-                     : folded;
+        uint32_t folded_g = fold_cursor();
         // (lane masks from single compares: see ballot_and)
-        const bool ring_ok = P == 1 || k < folded_g + kRing;
-        const bool can_start = mode == 0u && ring_ok;
-        const uint64_t pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
+        bool ring_ok = P == 1 || k < folded_g + kRing;
+        bool can_start = mode == 0u && ring_ok;
+        uint64_t pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         const uint64_t sec = __builtin_amdgcn_ballot_w64(mode == 1u);
         const uint64_t alive = __builtin_amdgcn_ballot_w64(mode != 2u) | (folding & __builtin_amdgcn_ballot_w64(folded < a.frames));
         if (alive == 0) break;
         const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
+        // Secondary segments run the full sphere loop; let them gather until
+        // enough lanes share one (or no primary work is ready).
+        const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        if (kFoldBeforePrimary && !do_sec) {
+            // the owners fold only before a primary round (or when nothing is left to
+            // trace): a secondary round starts no sample, so it needs no ring space
+            fold_ring();
+            folded_g = fold_cursor();
+            ring_ok = P == 1 || k < folded_g + kRing;
+            can_start = mode == 0u && ring_ok;
+            pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
+        }
         if ((pri | sec) != 0) {
-            // Secondary segments run the full sphere loop; let them gather until
-            // enough lanes share one (or no primary work is ready).
-            const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
             if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 if (do_sec && __builtin_popcountll(sec) < 16) { st_sparse_it += 1; st_sparse_lanes += __builtin_popcountll(sec); }
@@ -1226,30 +1268,7 @@ void trace_kernel(TraceArgs a) {
             const bool was_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
             (was_sec ? st_cyc_sec : st_cyc_pri) += st_t1 - st_t0;
         }
-        if (P > 1 && owner && valid) {
-            // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
-            // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
-            // sample's lane.  The fold is one sequential chain per pixel, so the owner
-            // reads kFoldBatch ring slots per LDS round trip (more for more lanes).
-            constexpr uint32_t kFoldBatch = P >= 8 ? 4u : 2u;
-            bool more = true;
-            while (more && folded < a.frames) {
-                float4 r[kFoldBatch];
-#pragma unroll
-                for (uint32_t i = 0; i < kFoldBatch; ++i) r[i] = ring[((folded + i) % kRing) * kRingStride];
-#pragma unroll
-                for (uint32_t i = 0; i < kFoldBatch; ++i) {
-                    more = more && folded < a.frames && __builtin_signbit(r[i].w);
-                    if (more) {
-                        accx = r[i].x + accx * -r[i].w;
-                        accy = r[i].y + accy * -r[i].w;
-                        accz = r[i].z + accz * -r[i].w;
-                        ring[(folded % kRing) * kRingStride].w = 0.0f;
-                        folded += 1u;
-                    }
-                }
-            }
-        }
+        if (!kFoldBeforePrimary) fold_ring();
         if (kStats && a.stats) st_cyc_fold += __builtin_amdgcn_s_memtime() - st_t1;
     }
 
