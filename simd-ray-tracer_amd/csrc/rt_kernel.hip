@@ -834,6 +834,10 @@ constexpr int kWavesPerBlock = 4;
 #define RTK_FOLD_BEFORE_PRIMARY 1
 #endif
 constexpr bool kFoldBeforePrimary = RTK_FOLD_BEFORE_PRIMARY != 0;
+#ifndef RTK_FOLD_LAZY  // 1: ... and only when a lane waits for ring space (A/B)
+#define RTK_FOLD_LAZY 1
+#endif
+constexpr bool kFoldLazy = RTK_FOLD_LAZY != 0;
 // primary group mask words per wave tile: the LDS-image kernels keep this
 // small (it is static LDS, and C2's blocks fill the CU's 160 KB 7 times)
 template <bool GS>
@@ -1098,7 +1102,10 @@ void trace_kernel(TraceArgs a) {
         // Secondary segments run the full sphere loop; let them gather until
         // enough lanes share one (or no primary work is ready).
         const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
-        if (kFoldBeforePrimary && !do_sec) {
+        // (lazy: only when some lane waits for ring space, or nothing else is left)
+        const bool fold_now = !do_sec && (!kFoldLazy || (pri | sec) == 0 ||
+                                          (__builtin_amdgcn_ballot_w64(mode == 0u) & ~pri) != 0);
+        if (kFoldBeforePrimary && fold_now) {
             // the owners fold only before a primary round (or when nothing is left to
             // trace): a secondary round starts no sample, so it needs no ring space
             fold_ring();
