@@ -847,9 +847,15 @@ struct MaskWords {
 constexpr uint32_t kFoldTable = 256;
 // Per-pixel out-of-order sample slots (LDS ring): at least P (every sample
 // lane holds one sample in flight) plus slack.
+#ifndef RTK_RING_SMALL_P  // ring slots per pixel for P <= 4 (A/B)
+#define RTK_RING_SMALL_P 16
+#endif
+#ifndef RTK_RING_PER_LANE  // ring slots per sample lane for P > 4 (A/B)
+#define RTK_RING_PER_LANE 2
+#endif
 template <int P>
 struct Ring {
-    static constexpr uint32_t N = P <= 4 ? 8u : 2u * (uint32_t)P;
+    static constexpr uint32_t N = P <= 4 ? (uint32_t)RTK_RING_SMALL_P : (uint32_t)RTK_RING_PER_LANE * (uint32_t)P;
 };
 
 #ifndef RTK_SOLO_WAVES_PER_SIMD  // the same target for the one-wave kernels (A/B: make variant KFLAGS=-DRTK_SOLO_WAVES_PER_SIMD=8)
