@@ -850,6 +850,9 @@ constexpr uint32_t kFoldTable = 256;
 #ifndef RTK_RING_SMALL_P  // ring slots per pixel for P <= 4 (A/B)
 #define RTK_RING_SMALL_P 16
 #endif
+#ifndef RTK_FOLD_BATCH_SMALL_P  // ring slots the owner reads per LDS round trip at P <= 4 (A/B)
+#define RTK_FOLD_BATCH_SMALL_P 2
+#endif
 #ifndef RTK_RING_PER_LANE  // ring slots per sample lane for P > 4 (A/B)
 #define RTK_RING_PER_LANE 2
 #endif
@@ -1072,7 +1075,7 @@ void trace_kernel(TraceArgs a) {
             // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
             // sample's lane.  The fold is one sequential chain per pixel, so the owner
             // reads kFoldBatch ring slots per LDS round trip (more for more lanes).
-            constexpr uint32_t kFoldBatch = P >= 8 ? 4u : 2u;
+            constexpr uint32_t kFoldBatch = P >= 8 ? 4u : (uint32_t)RTK_FOLD_BATCH_SMALL_P;
             bool more = true;
             while (more && folded < a.frames) {
                 float4 r[kFoldBatch];
