@@ -243,7 +243,10 @@ def main():
     # ends only after the last frame is assembled on rank 0.
     cur = [torch.zeros(maxr * W, dtype=torch.int32, device="cuda") for _ in range(2)]
     prev = torch.zeros((maxr * W, 4), dtype=torch.float32, device="cuda")
-    rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    rays = torch.zeros(1, dtype=torch.int64, device="cuda")  # the tiny code-object launch's counter
+    # one pre-zeroed ray counter per step (cold, warm-ups, timed): no counter
+    # reset between launches, and every timed step's count is checked after
+    ctr = torch.zeros(args.warmup + args.steps + 2, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream()
     comm, gather_kind = None, None
     if world > 1:
@@ -275,7 +278,7 @@ def main():
     side = torch.cuda.Stream() if comm else None
     gathered = [None, None]  # per slot: event after its gather on the side stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    state = {"n": 0, "pending": None}
+    state = {"n": 0, "pending": None, "c": 0}
 
     def finish():  # frame whose gather is in flight -> assembled on rank 0
         if state["pending"] is None:
@@ -293,11 +296,12 @@ def main():
         state["n"] += 1
         if gathered[slot] is not None:  # the gather two frames back has read this slot
             stream.wait_event(gathered[slot])
-        rays.zero_()
+        c = state["c"]
+        state["c"] += 1
         if i is not None:
             ev[i][0].record(stream)
         dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur[slot].data_ptr(),
-                  rays_ptr=rays.data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
+                  rays_ptr=ctr[c].data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
                   band_rows=band_rows, band_count=bands, band_index=band_index, accum_zero=True,
                   stream=stream.cuda_stream)
         if i is not None:
@@ -338,7 +342,9 @@ def main():
         step()
     finish()
     torch.cuda.synchronize()
-    rays_per_step = torch.tensor([int(rays.item()), dev.last_info()["SegmentsFolded"]], dtype=torch.int64,
+    rays_local = int(ctr[state["c"] - 1].item())  # this rank's segments per launch (last warm-up)
+    first_timed = state["c"]
+    rays_per_step = torch.tensor([rays_local, dev.last_info()["SegmentsFolded"]], dtype=torch.int64,
                                  device="cuda")
     if world > 1:
         dist.all_reduce(rays_per_step)
@@ -353,6 +359,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     info = dev.last_info()
+    timed_counts = ctr[first_timed:first_timed + args.steps].tolist()
+    if any(n != rays_local for n in timed_counts):
+        raise SystemExit(f"bench.py: timed steps counted {timed_counts} segments, expected {rays_local} each")
     verified = None
     if args.verify and bands == world:  # rank 0 renders the whole frame alone and compares
         if rank == 0:
@@ -380,7 +389,7 @@ def main():
         if rank == 0:
             out = {"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
                    "rank0_kernel_ms": round(kern_ms, 3), "lanes_per_pixel": info["LanesPerPixel"],
-                   "rank0_rays": int(rays.item()), "ms_per_step": round(elapsed / args.steps * 1e3, 3)}
+                   "rank0_rays": rays_local, "ms_per_step": round(elapsed / args.steps * 1e3, 3)}
             stats = dev.debug_stats()
             if stats:
                 out["sched_stats"] = stats
@@ -390,7 +399,6 @@ def main():
         dev.close()
         return
     if rank == 0:
-        rays_local = int(rays.item())  # rank 0's rays per launch
         ops = rays_local * ops_per_segment(N)
         achieved_alg = ops / (kern_ms / 1e3) / 1e12
         fb_bytes = rows[0] * W * (16 + 4)  # accumulation + RGBA8 written once per launch
@@ -444,6 +452,7 @@ def main():
                        **({"gather": gather_kind} if world > 1 else {}),
                        "rays_per_step": seg_counted},
             "segments": {"counted_per_step": seg_counted, "traced_per_step": seg_traced,
+                         "counted_equal_every_timed_step": True,  # one counter per step, checked above
                          "folded_per_step": seg_folded,
                          "traced_mrays_per_s": round(seg_traced * args.steps / elapsed / 1e6, 1),
                          "note": "every segment is counted as the reference counts it (main.cpp:390); 'folded' "
