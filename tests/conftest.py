@@ -36,13 +36,46 @@ def pytest_configure(config):
                                                str(MULTIRANK_OUT)], cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
 
 
+    # the plain-C host (examples/c_host/render) on one device and on three
+    # bands of the same device, also started before this process touches the
+    # GPU; tests/test_c_host.py compares its frames with the oracle's
+    if _selects_gpu(config) and C_HOST_BIN.exists():
+        import subprocess
+        C_HOST_OUT.mkdir(parents=True, exist_ok=True)
+        for name, devs in C_HOST_RUNS.items():
+            for old in C_HOST_OUT.glob(name + ".*"):
+                old.unlink()
+            log = open(C_HOST_OUT / (name + ".log"), "w")
+            _c_host[name] = subprocess.Popen([str(C_HOST_BIN), str(C_HOST_W), str(C_HOST_H), str(C_HOST_FRAMES),
+                                              str(C_HOST_SCENE), str(C_HOST_OUT / name), devs],
+                                             cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
+
+
 def pytest_unconfigure(config):
-    p = _multirank.get("proc")
-    if p is not None and p.poll() is None:
-        try:
-            p.wait(timeout=300)
-        except Exception:
-            p.kill()
+    for p in [_multirank.get("proc")] + list(_c_host.values()):
+        if p is not None and p.poll() is None:
+            try:
+                p.wait(timeout=300)
+            except Exception:
+                p.kill()
+
+
+C_HOST_BIN = ROOT / "examples" / "c_host" / "render"
+C_HOST_OUT = ROOT / "gpurun_out" / "c_host"
+C_HOST_RUNS = {"one_device": "0", "three_bands": "0,0,0"}
+C_HOST_W, C_HOST_H, C_HOST_FRAMES, C_HOST_SCENE = 72, 40, 3, 0
+_c_host = {}
+
+
+@pytest.fixture(scope="session")
+def c_host_runs():
+    """{run name: (exit code, output prefix)} of the plain-C host runs (waits for them)."""
+    if not _c_host:
+        pytest.skip("C host runs not started (run with -m gpu after build())")
+    out = {}
+    for name, p in _c_host.items():
+        out[name] = (p.wait(timeout=280), C_HOST_OUT / name)
+    return out
 
 
 @pytest.fixture(scope="session")
