@@ -1467,6 +1467,7 @@ __global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t 
     a.cur[pix] = rgba8(accx, accy, accz, (a.flags & kFlagSrgbPow) != 0u);
 }
 
+#ifndef RTK_P16_TU  // (the P = 16 translation unit holds only its trace launches: see launch_p16)
 // Scatter RCCL-gathered compact band images into the full framebuffer.
 __global__ __launch_bounds__(256) void assemble_kernel(const uint8_t *src, uint64_t rank_stride, uint8_t *dst,
                                                        uint32_t width, uint32_t height, uint32_t elem,
@@ -1611,8 +1612,10 @@ __global__ __launch_bounds__(kSortBlock) void tile_rank_kernel(uint32_t *cost, u
     }
 }
 
+#endif  // !RTK_P16_TU
 }  // namespace rtk
 
+#ifndef RTK_P16_TU
 extern "C" size_t rtk_tile_sort_scratch(uint32_t n) {
     return rtk::kSortBuckets * 4u * (size_t)((n + rtk::kSortBlock - 1u) / rtk::kSortBlock);
 }
@@ -1643,6 +1646,8 @@ extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lane
     }
     return ((width + bw - 1u) / bw) * ((local_rows + bh - 1u) / bh);
 }
+
+#endif  // !RTK_P16_TU
 
 template <int P>
 static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks, hipStream_t stream) {
@@ -1704,12 +1709,26 @@ static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n
 #undef RTK_LAUNCH
 }
 
+// The P = 16 trace kernels (the 8-GPU band shares) are compiled in
+// a translation unit of their own (this file with RTK_P16_TU, Makefile
+// build/rt_kernel_p16.o) under the scheduler's register-pressure trackers
+// (-amdgpu-use-amdgpu-trackers): about -1.4 % on the 8-rank share over two same-box
+// A/Bs (0.770 against 0.781 ms, near the noise), while the same flag
+// costs the P = 4 kernel of one GPU 1.7 % (profiles/r02_sched_trackers_ab.txt).
+extern "C" void rtk_launch_p16(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks,
+                               hipStream_t stream);
+#ifdef RTK_P16_TU
+extern "C" void rtk_launch_p16(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks,
+                               hipStream_t stream) {
+    launch_p<16>(a, simd, src, cull, n_blocks, stream);
+}
+#else
 extern "C" int rtk_launch_trace_grid(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
                                      uint32_t n_blocks, hipStream_t stream) {
     if (n_blocks == 0) return 0;
     switch (lanes_per_pixel) {
         case 32: launch_p<32>(a, simd, src, cull, n_blocks, stream); break;
-        case 16: launch_p<16>(a, simd, src, cull, n_blocks, stream); break;
+        case 16: rtk_launch_p16(a, simd, src, cull, n_blocks, stream); break;
         case 8: launch_p<8>(a, simd, src, cull, n_blocks, stream); break;
         case 4: launch_p<4>(a, simd, src, cull, n_blocks, stream); break;
         case 2: launch_p<2>(a, simd, src, cull, n_blocks, stream); break;
@@ -1804,3 +1823,4 @@ extern "C" int rtk_launch_assemble(const void *src, uint64_t rank_stride, void *
                        width, height, elem, band_rows, band_count);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+#endif  // RTK_P16_TU
