@@ -66,7 +66,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", choices=sorted(CONFIGS), default="c2", help="BASELINE.json workload preset")
+    p.add_argument("--config", choices=sorted(CONFIGS) + ["onrender"], default="c2",
+                   help="BASELINE.json workload preset; 'onrender': the reference's per-frame OnRender loop")
     p.add_argument("--width", type=int)
     p.add_argument("--height", type=int)
     p.add_argument("--spp", type=int)
@@ -85,7 +86,14 @@ def parse():
                    help="diagnostic (1 GPU): trace only band residue --sim-index of this many ranks, i.e. one rank's "
                         "share of a multi-GPU frame; prints that rank's kernel time, not a bench line")
     p.add_argument("--sim-index", type=int, default=0, help="band residue (rank) traced by --sim-ranks")
+    p.add_argument("--devices", help="HIP devices of a single-process multi-GPU run (default 0..N-1)")
+    p.add_argument("--transport", choices=("auto", "rccl", "peer"), default="auto",
+                   help="single-process multi-GPU gather: RCCL, peer copies, or RCCL where it can be used")
+    p.add_argument("--no-verify", action="store_true", help="multi-GPU: skip the whole-frame check (on by default)")
+    p.add_argument("--frames", type=int, default=256, help="onrender: completed frames per measured run")
     a = p.parse_args()
+    if a.config == "onrender":
+        return a
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
@@ -156,15 +164,16 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def pmc_record(workload: str):
-    """The newest committed rocprofv3 --pmc record of this workload
-    (profiles/rNN_*_pmc.json, written by scripts/pmc_to_json.py)."""
+def pmc_record(workload: str, bands: int = 1):
+    """The newest committed rocprofv3 --pmc record of this workload and band
+    split (profiles/rNN_*_pmc.json, written by scripts/pmc_to_json.py; a
+    record without "bands" is a whole-frame, one-GPU one)."""
     for f in sorted((ROOT / "profiles").glob("r*_pmc.json"), reverse=True):
         try:
             rec = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if rec.get("workload") == workload:
+        if rec.get("workload") == workload and int(rec.get("bands", 1)) == bands:
             rec["file"] = f"profiles/{f.name}"
             return rec
     return None
@@ -180,34 +189,346 @@ def valu_roofline(pmc, kern_ms: float):
     pair, and SQ_ACTIVE_INST_VALU2 counts the quad-cycles in which two issued.
     So a SIMD's VALU is occupied for ACTIVE_INST_VALU - ACTIVE_INST_VALU2
     quad-cycles, out of cycles/4:
-        frac = (ACTIVE_INST_VALU - ACTIVE_INST_VALU2) / (1024 SIMDs x cycles / 4)
-    (<= 1: a VALU-bound kernel reaches 1 when every SIMD issues every
-    quad-cycle).  One quad-cycle slot is the capacity of 128 f32 add/mul lane
-    ops (a dual-issued wave64 pair, or one v_pk_*_f32), so `achieved` =
-    slots x 128 / live kernel time is in f32 add/mul-equivalent TFLOP/s
-    against the 78.6 T peak."""
+        frac      = (ACTIVE_INST_VALU - ACTIVE_INST_VALU2) / (1024 SIMDs x cycles / 4)
+                    (VALU issue occupancy, <= 1)
+        lane_util = THREAD_CYCLES_VALU / (64 x ACTIVE_INST_VALU)
+        frac_lane = frac x lane_util   (the share of issue capacity doing useful lanes)
+        achieved  = INSTS_VALU_FLOPS_FP32 x 64 x lane_util / kernel time   (f32 lane flops/s;
+                    the counter counts per wave instruction, 2 per FMA, packed ops per element)
+        issue_capacity_tops = (ACTIVE_INST_VALU - ACTIVE_INST_VALU2) x 128 / kernel time
+                    (one quad-cycle slot = 128 f32 add/mul lane-op capacity)"""
     c = pmc["counters_per_dispatch"]
     cycles = pmc["gpu_cycles_per_dispatch"]
     slots = c["SQ_ACTIVE_INST_VALU"] - c["SQ_ACTIVE_INST_VALU2"]
     frac = slots / (SIMDS * cycles / 4.0)
-    return {"frac": round(frac, 4), "achieved": round(slots * 128 / (kern_ms / 1e3) / 1e12, 2),
-            "valu_slots_per_launch": slots,
-            "valu_instructions_per_launch": c["SQ_INSTS_VALU"],
-            "dual_issue_share": round(2 * c["SQ_ACTIVE_INST_VALU2"] / c["SQ_ACTIVE_INST_VALU"], 4),
-            "lane_utilisation": round(c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"]), 4),
-            "wave_cycles_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4),
-            "salu_per_valu": round(c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"], 4),
-            "gpu_cycles_per_launch": cycles}
+    lane = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
+    flops = c["SQ_INSTS_VALU_FLOPS_FP32"] * 64.0 * lane
+    sec = kern_ms / 1e3
+    out = {"frac": round(frac, 4), "frac_lane": round(frac * lane, 4),
+           "achieved": round(flops / sec / 1e12, 2), "issue_capacity_tops": round(slots * 128 / sec / 1e12, 2),
+           "valu_slots_per_launch": slots,
+           "valu_instructions_per_launch": c["SQ_INSTS_VALU"],
+           "f32_lane_flops_per_launch": round(flops),
+           "dual_issue_share": round(2 * c["SQ_ACTIVE_INST_VALU2"] / c["SQ_ACTIVE_INST_VALU"], 4),
+           "lane_utilisation": round(lane, 4),
+           "wave_cycles_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4),
+           "salu_per_valu": round(c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"], 4),
+           "gpu_cycles_per_launch": cycles}
+    if "SQ_ACTIVE_INST_SCA" in c and "SQ_BUSY_CYCLES" in c:
+        # scalar unit: one per CU (256), SQ_ACTIVE_INST_SCA in quad-cycles like the VALU counter
+        out["salu_issue_occupancy"] = round(c["SQ_ACTIVE_INST_SCA"] / (256 * cycles / 4.0), 4)
+    return out
+
+
+def workload_name(args, W, H, S, N, B) -> str:
+    preset = all(getattr(args, k) == v for k, v in CONFIGS[args.config].items())
+    tag = args.config.upper() if preset else "custom"
+    view = "" if args.distance is None else f", camera {args.distance:g} from look-at"
+    return (f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
+            + ("" if args.scene == 1 else f", {SCENE_NAMES[args.scene]}") + view)
+
+
+def roofline(args, info, kern_ms: float, rays_local: int, rows0: int, W: int, N: int, workload: str, bands: int):
+    """The dominant kernel's roofline object (one device's trace kernel)."""
+    ops = rays_local * ops_per_segment(N)
+    achieved_alg = ops / (kern_ms / 1e3) / 1e12
+    fb_bytes = rows0 * W * (16 + 4)  # accumulation + RGBA8 written once per launch
+    hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
+    pmc = pmc_record(workload, bands)
+    walks = {0: "any", 1: "groups", 2: "cl1", 3: "cl2", 4: "cl4", 5: "cl1rel", 6: "cl2rel", 7: "cl4rel"}
+    kernel = (f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{info['LanesPerPixel']},"
+              f"{'one-wave' if info['OneWaveGroups'] else 'four-wave'},walk={walks.get(info['Walk'], '?')}>")
+    roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1), "unit": "TFLOP/s",
+            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": round(kern_ms, 3)}
+    if pmc:
+        ex = valu_roofline(pmc, kern_ms)
+        roof["achieved"], roof["frac"] = ex.pop("achieved"), ex.pop("frac")
+        roof["frac_lane"] = ex.pop("frac_lane")
+        roof["frac_flops"] = round(roof["achieved"] / VALU_PEAK_TOPS, 4)
+        roof["issue_capacity_tops"] = ex.pop("issue_capacity_tops")
+        roof["traffic"] = round(pmc["hbm_bytes_per_dispatch"]) if "hbm_bytes_per_dispatch" in pmc else None
+        roof["executed"] = ex
+        roof["source"] = pmc["file"]
+        roof["note"] = ("frac = VALU issue occupancy of the trace kernel from the committed PMC record: "
+                        "(SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4); "
+                        "frac_lane = frac x lane utilisation (SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)); "
+                        "achieved = f32 lane flops = SQ_INSTS_VALU_FLOPS_FP32 x 64 x lane utilisation / live kernel "
+                        "ms, against the 78.6 T f32 add/mul peak (frac_flops; the FMA-counted spec is 157.3 T); "
+                        "issue_capacity_tops = issued quad-cycle slots x 128 / kernel ms (bench.py valu_roofline). "
+                        "traffic = FETCH_SIZE x2 + WRITE_SIZE (KiB), per launch.")
+    roof["frac_algorithmic"] = round(achieved_alg / VALU_PEAK_TOPS, 4)
+    roof["achieved_algorithmic"] = round(achieved_alg, 2)
+    roof["work_per_launch"] = (f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d brute force; the "
+                               "kernel skips most sphere tests exactly, so this rate can exceed the peak)")
+    roof["hbm"] = {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}
+    return roof
+
+
+def base_line(args, *, world, elapsed, seg_counted, seg_folded, W, H, S, N, B, workload, parallelism, gather=None):
+    value = seg_counted * args.steps / elapsed / 1e6
+    seg_traced = seg_counted - seg_folded
+    return {
+        "metric": f"Mrays/sec at {W}x{H}, {S}spp, {B} bounces, {N} spheres",
+        "value": round(value, 1),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic ({'first ' + str(N) + ' spheres of ' if args.scene == 1 else ''}the reference's "
+                f"{SCENE_NAMES[args.scene]} scene, {'default camera' if args.distance is None else 'camera moved'}"
+                ", per-(pixel,frame) PCG seeds)",
+        "config": {"workload": workload,
+                   "width": W, "height": H, "spp": S, "spheres": N, "bounces": B, "scene": args.scene,
+                   "parallelism": parallelism,
+                   **({"gather": gather} if gather else {}),
+                   "rays_per_step": seg_counted},
+        "segments": {"counted_per_step": seg_counted, "traced_per_step": seg_traced,
+                     "counted_equal_every_timed_step": True,  # one counter per step, checked by the caller
+                     "folded_per_step": seg_folded,
+                     "traced_mrays_per_s": round(seg_traced * args.steps / elapsed / 1e6, 1),
+                     "note": "every segment is counted as the reference counts it (main.cpp:390); 'folded' "
+                             "ones belong to pixels whose every sample provably misses (dead tiles), folded "
+                             "by the empty-tile kernel instead of traced"},
+    }
+
+
+def one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, steps: int):
+    """The whole frame on one device alone (multi-GPU lines): its RGBA8 frame
+    (the --verify reference) and its ms per frame over `steps` warm launches."""
+    cur = torch.zeros(H * W, dtype=torch.int32, device=torch.cuda.current_device())
+    prev = torch.zeros((H * W, 4), dtype=torch.float32, device=torch.cuda.current_device())
+    ctr = torch.zeros(steps + 3, dtype=torch.int64, device=torch.cuda.current_device())
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for i in range(steps + 3):
+        if i == 3:
+            torch.cuda.synchronize()
+            ev[0].record(stream)
+        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                  rays_ptr=ctr[i].data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
+                  band_rows=args.band_rows, band_count=1, band_index=0, accum_zero=True, stream=stream.cuda_stream)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    return cur, ev[0].elapsed_time(ev[1]) / steps, int(ctr[steps + 2].item())
+
+
+def main_multi_device(args):
+    """--gpus N (N > 1) without a launcher: ONE process drives N devices through
+    the C-ABI's rt_multi (include/rt_trace.h): interleaved 8-row bands dealt
+    over the devices, each traced on its own stream, RCCL grouped send/recv to
+    devices[0] (ncclCommInitAll; peer copies where RCCL cannot be used, e.g. a
+    device listed twice) and the assembly -- all inside the timed region.  The
+    reference drives its worker pool from one process the same way
+    (main.cpp:851-856, wasm/wasm.cpp:651-678)."""
+    import torch
+    import __graft_entry__ as graft
+
+    rt = graft.load_package()
+    if os.environ.get("BENCH_SHARE_GPU") == "1":
+        devices = [0] * args.gpus
+    elif args.devices:
+        devices = [int(d) for d in args.devices.split(",")]
+    else:
+        devices = list(range(args.gpus))
+    if len(devices) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but --devices lists {len(devices)}")
+    visible = torch.cuda.device_count()  # does not initialise the GPU
+    if visible < max(devices) + 1:
+        print(f"bench.py: --gpus {args.gpus} needs HIP devices {sorted(set(devices))}, but {visible} "
+              f"{'is' if visible == 1 else 'are'} visible (set BENCH_SHARE_GPU=1 to deal the bands over one "
+              "device, or launch one process per GPU with torch.distributed.run)", file=sys.stderr)
+        raise SystemExit(2)
+    d0 = devices[0]
+    torch.cuda.set_device(d0)
+    scene = make_scene(rt, args)
+    W, H, S, B, N = args.width, args.height, args.spp, args.bounces, args.spheres
+    cam = rt.camera_setup(scene, W, H, distance=args.distance)
+    transport = rt.RT_MULTI_PEER if args.transport == "peer" else rt.RT_MULTI_RCCL if args.transport == "rccl" \
+        else rt.RT_MULTI_AUTO
+    multi = rt.Multi(devices, transport=transport)
+    multi.upload_scene(scene)
+    full = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    ctr = torch.zeros(args.warmup + args.steps + 2, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream()
+    tiny = torch.zeros(64 * 8, dtype=torch.int32, device="cuda")
+    tiny_rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+    band_rows = args.band_rows
+
+    def call(c):
+        multi.trace(cam, width=W, height=H, cur_ptr=full.data_ptr(), rays_ptr=ctr[c].data_ptr(), frames=S,
+                    max_bounce=B, simd=not args.scalar, band_rows=band_rows, accum_zero=True,
+                    stream=stream.cuda_stream)
+
+    # code objects on every device (a tiny frame), then the cold call of this geometry
+    multi.trace(cam, width=64, height=8 * len(devices), cur_ptr=torch.zeros(64 * 8 * len(devices), dtype=torch.int32,
+                device="cuda").data_ptr(), rays_ptr=tiny_rays.data_ptr(), frames=1, max_bounce=1,
+                simd=not args.scalar, band_rows=8, accum_zero=True, stream=stream.cuda_stream)
+    multi.synchronize()
+    del tiny
+    t = time.perf_counter()
+    call(0)
+    multi.synchronize()
+    cold_ms = (time.perf_counter() - t) * 1e3
+    for c in range(1, args.warmup):
+        call(c)
+    multi.synchronize()
+    c_last = max(args.warmup - 1, 0)
+    rays_per_step = int(ctr[c_last].item())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        call(args.warmup + i)
+        ev[i][1].record(stream)
+    multi.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timed = ctr[args.warmup:args.warmup + args.steps].tolist()
+    if any(n != rays_per_step for n in timed):
+        raise SystemExit(f"bench.py: timed steps counted {timed} segments, expected {rays_per_step} each")
+    per_dev_ms = multi.last_trace_ms(len(devices))
+    minfo = multi.info()
+    call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    frame = full.clone()
+    # the whole frame on devices[0] alone: the 1-GPU time on this box and the --verify reference
+    dev = rt.Device(d0)
+    dev.upload_scene(scene)
+    ref, one_ms, one_rays = one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, min(args.steps, 5))
+    one_info = dev.last_info()
+    verified = bool(torch.equal(frame, ref)) and one_rays == rays_per_step
+    workload = workload_name(args, W, H, S, N, B)
+    gather = ("RCCL grouped send/recv to devices[0] (ncclCommInitAll) + rt_assemble scatter, overlapping the next "
+              "call's traces" if minfo["Transport"] == rt.RT_MULTI_RCCL else
+              "hipMemcpyPeerAsync to devices[0] + rt_assemble scatter, overlapping the next call's traces")
+    elapsed_share = elapsed
+    line = base_line(args, world=args.gpus, elapsed=elapsed_share, seg_counted=rays_per_step,
+                     seg_folded=minfo["SegmentsFolded"], W=W, H=H, S=S, N=N, B=B, workload=workload,
+                     parallelism=f"{args.gpus} GPU x interleaved {band_rows}-row bands, one process (rt_multi)",
+                     gather=gather)
+    line["config"]["launcher"] = "single process: rt_multi over devices " + ",".join(map(str, devices))
+    line["config"]["devices"] = devices
+    line["cold_ms"] = round(cold_ms, 3)
+    line["cold"] = {"ms": round(cold_ms, 3), "note": "first call for this camera/geometry on every device (cull "
+                    "passes + untrained tile orders + RCCL/peer setup), wall clock incl. its synchronisation"}
+    line["per_device_trace_ms"] = [round(v, 3) for v in per_dev_ms]
+    line["call_ms_events"] = round(call_ms, 3)
+    line["one_gpu"] = {"ms_per_frame": round(one_ms, 3), "device": d0,
+                       "speedup_vs_one_gpu": round(one_ms / (elapsed / args.steps * 1e3), 3),
+                       "note": "the same frame traced whole on devices[0] alone, in this run"}
+    line["verified"] = verified
+    # the roofline of the slowest device's share (its trace kernel; counters: the committed share record)
+    slowest = max(range(len(devices)), key=lambda i: per_dev_ms[i])
+    rows0 = rt.band_local_rows(H, band_rows, args.gpus, slowest)
+    share_info = {"LanesPerPixel": 16 if rows0 * W < 256 * 1536 else 8 if rows0 * W < 256 * 6144 else 4,
+                  "OneWaveGroups": one_info["OneWaveGroups"], "Walk": one_info["Walk"]}
+    line["roofline"] = roofline(args, share_info, per_dev_ms[slowest], rays_per_step // args.gpus, rows0, W, N,
+                                workload, args.gpus)
+    line["roofline"]["device"] = slowest
+    print(json.dumps(line), flush=True)
+    dev.close()
+    multi.close()
+
+
+def main_onrender(args):
+    """The reference's own per-frame unit: OnRender (main.cpp:705-859), called
+    by the platform once per animation frame (wasm/wasm.cpp:176-218) with one
+    progressive sample per pixel per call, MaxBounce 5 (main.cpp:387), the
+    completed frame handed back one call late.  Driven here through the C-ABI
+    (rt_on_init / rt_on_init_devices + rt_on_render, busy-polling like a
+    platform loop with a GPU behind it) at 1920x1080 and at 960x540 (the
+    default 1280x720 window x the 0.75 render scale, main.cpp:649-650,
+    wasm/wasm.cpp:78), scene 0 (RGB Glass, wasm/wasm.cpp:20) unless --scene:
+      static: the camera stays, so every call folds one more frame;
+      moving: RT_KEY_LEFT on every call (main.cpp:743-746), so every frame
+              restarts the mean, re-runs the cull pass, and waits for the
+              previous frame (WorkQueueWaitUntilCompletion, main.cpp:792).
+    The line reports Mrays/s and ms per completed frame for each, and where
+    the host time went (rt_on_render_get_profile)."""
+    import numpy as np
+    import torch
+    import __graft_entry__ as graft
+
+    rt = graft.load_package()
+    if os.environ.get("BENCH_SHARE_GPU") == "1":
+        devices = [0] * args.gpus
+    elif args.devices:
+        devices = [int(d) for d in args.devices.split(",")]
+    else:
+        devices = list(range(args.gpus))
+    visible = torch.cuda.device_count()
+    if visible < max(devices) + 1:
+        print(f"bench.py: onrender over devices {sorted(set(devices))} but {visible} visible", file=sys.stderr)
+        raise SystemExit(2)
+    scene = 0 if args.scene is None else args.scene
+    sizes = [(args.width, args.height)] if args.width and args.height else [(1920, 1080), (960, 540)]
+    device_sets = [devices[:1]] + ([devices] if len(devices) > 1 else [])
+    has_profile = hasattr(rt.lib(), "rt_on_render_get_profile")
+    runs = []
+    for devs in device_sets:
+        for (W, H) in sizes:
+            for mode, keys in (("static", 0), ("moving", rt.KEY_LEFT)):
+                rt.on_init(devs if len(devs) > 1 else None)
+                img = np.zeros((H, W), np.uint32)
+                warm = 0
+                while warm < 8:  # code objects, allocations, the first cull pass
+                    ok, _, _ = rt.on_render(img, scene, True, keys)
+                    warm += int(ok)
+                if has_profile:
+                    rt.on_render_profile(reset=True)
+                done = rays = calls = 0
+                t0 = time.perf_counter()
+                while done < args.frames:
+                    ok, r, _ = rt.on_render(img, scene, True, keys)
+                    calls += 1
+                    if ok:
+                        done += 1
+                        rays += r
+                wall = time.perf_counter() - t0
+                run = {"devices": devs, "width": W, "height": H, "mode": mode, "frames": done, "calls": calls,
+                       "rays": rays, "mrays_per_s": round(rays / wall / 1e6, 1),
+                       "ms_per_frame": round(wall / done * 1e3, 4)}
+                if has_profile:
+                    prof = rt.on_render_profile()
+                    wall_ms = wall * 1e3
+                    run["host_ms_per_frame"] = {k: round(prof[k] / done, 4) for k in
+                                                ("CallMs", "HostCopyMs", "HostWaitMs")}
+                    run["gpu_ms_per_frame"] = round(prof["GpuFrameMs"] / max(prof["FramesCopied"], 1), 4)
+                    run["share_of_wall"] = {"host_copy": round(prof["HostCopyMs"] / wall_ms, 4),
+                                            "host_wait": round(prof["HostWaitMs"] / wall_ms, 4),
+                                            "gpu_frame": round(prof["GpuFrameMs"] / wall_ms, 4)}
+                rt.on_shutdown()
+                runs.append(run)
+                print(json.dumps(run), file=sys.stderr, flush=True)
+    line = {"metric": "OnRender Mrays/sec (1 spp per call, 5 bounces)", "value": runs[0]["mrays_per_s"],
+            "unit": "Mrays/s", "n_gpus": len(set(devices)) if len(devices) > 1 else 1, "steps": args.frames,
+            "warmup": 8, "ms_per_step": runs[0]["ms_per_frame"], "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32",
+            "data": f"the reference's built-in scene {scene} ({SCENE_NAMES[scene]}), its default camera",
+            "config": {"workload": "onrender", "scene": scene, "lib": os.environ.get("RT_TRACE_LIB", "librt_trace.so"),
+                       "note": "value/ms_per_step: the first run (1 device, static camera, "
+                               f"{sizes[0][0]}x{sizes[0][1]}); every run is in 'runs'"},
+            "runs": runs}
+    print(json.dumps(line), flush=True)
 
 
 def main():
     args = parse()
+    if args.config == "onrender":
+        return main_onrender(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1 and args.sim_ranks == 0:
+        return main_multi_device(args)
     import torch
     import torch.distributed as dist
     import __graft_entry__ as graft
 
     rt = graft.load_package()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -362,16 +683,12 @@ def main():
     timed_counts = ctr[first_timed:first_timed + args.steps].tolist()
     if any(n != rays_local for n in timed_counts):
         raise SystemExit(f"bench.py: timed steps counted {timed_counts} segments, expected {rays_local} each")
-    verified = None
-    if args.verify and bands == world:  # rank 0 renders the whole frame alone and compares
+    verified, one_ms = None, None
+    if (args.verify or world > 1) and not args.no_verify and bands == world:
+        # rank 0 renders the whole frame alone: the 1-GPU time and the reference the gathered frame must equal
         if rank == 0:
-            ref_cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-            ref_prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
-            ref_rays = torch.zeros(1, dtype=torch.int64, device="cuda")
-            dev.trace(cam, width=W, height=H, prev_ptr=ref_prev.data_ptr(), cur_ptr=ref_cur.data_ptr(),
-                      rays_ptr=ref_rays.data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
-                      band_rows=band_rows, band_count=1, band_index=0, accum_zero=True, stream=stream.cuda_stream)
-            torch.cuda.synchronize()
+            ref_cur, one_ms, one_rays = one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream,
+                                                          min(args.steps, 5))
             got = full if world > 1 else cur[(state["n"] - 1) % 2]
             verified = bool(torch.equal(got, ref_cur))
         if world > 1:
@@ -383,13 +700,13 @@ def main():
     elapsed, kern_ms_max, cold_ms = float(t[0]), float(t[1]), float(t[2])
     seg_counted, seg_folded = int(rays_per_step[0].item()), int(rays_per_step[1].item())
     total_rays = seg_counted * args.steps
-    value = total_rays / elapsed / 1e6
 
     if bands != world:
         if rank == 0:
             out = {"sim_ranks": bands, "sim_index": band_index, "rank0_rows": rows[band_index],
                    "rank0_kernel_ms": round(kern_ms, 3), "lanes_per_pixel": info["LanesPerPixel"],
-                   "rank0_rays": rays_local, "ms_per_step": round(elapsed / args.steps * 1e3, 3)}
+                   "rank0_rays": rays_local, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                   "cold_ms": round(cold_ms, 3)}
             stats = dev.debug_stats()
             if stats:
                 out["sched_stats"] = stats
@@ -399,72 +716,24 @@ def main():
         dev.close()
         return
     if rank == 0:
-        ops = rays_local * ops_per_segment(N)
-        achieved_alg = ops / (kern_ms / 1e3) / 1e12
-        fb_bytes = rows[0] * W * (16 + 4)  # accumulation + RGBA8 written once per launch
-        hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
-        preset = all(getattr(args, k) == v for k, v in CONFIGS[args.config].items())
-        tag = args.config.upper() if preset else "custom"
-        view = "" if args.distance is None else f", camera {args.distance:g} from look-at"
-        workload = (f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
-                    + ("" if args.scene == 1 else f", {SCENE_NAMES[args.scene]}") + view)
-        pmc = pmc_record(workload)
-        walks = {0: "any", 1: "groups", 2: "cl1", 3: "cl2", 4: "cl4", 5: "cl1rel", 6: "cl2rel", 7: "cl4rel"}
-        kernel = (f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{info['LanesPerPixel']},"
-                  f"{'one-wave' if info['OneWaveGroups'] else 'four-wave'},walk={walks.get(info['Walk'], '?')}>")
-        roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1), "unit": "TFLOP/s",
-                "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": round(kern_ms, 3)}
-        if pmc:
-            ex = valu_roofline(pmc, kern_ms)
-            roof["achieved"], roof["frac"] = ex.pop("achieved"), ex.pop("frac")
-            roof["traffic"] = round(pmc["hbm_bytes_per_dispatch"]) if "hbm_bytes_per_dispatch" in pmc else None
-            roof["executed"] = ex
-            roof["source"] = pmc["file"]
-            roof["note"] = ("frac = VALU issue occupancy of the trace kernel from the committed PMC record: "
-                            "(SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4); "
-                            "achieved = those quad-cycle slots x 128 f32 lane-ops / live kernel ms "
-                            "(bench.py valu_roofline). traffic = FETCH_SIZE x2 + WRITE_SIZE (KiB), per launch.")
-        roof["frac_algorithmic"] = round(achieved_alg / VALU_PEAK_TOPS, 4)
-        roof["achieved_algorithmic"] = round(achieved_alg, 2)
-        roof["work_per_launch"] = (f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d brute force; the "
-                                   "kernel skips most sphere tests exactly, so this rate can exceed the peak)")
-        roof["hbm"] = {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}
-        seg_traced = seg_counted - seg_folded
-        line = {
-            "metric": f"Mrays/sec at {W}x{H}, {S}spp, {B} bounces, {N} spheres",
-            "value": round(value, 1),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": f"synthetic ({'first ' + str(N) + ' spheres of ' if args.scene == 1 else ''}the reference's "
-                    f"{SCENE_NAMES[args.scene]} scene, {'default camera' if args.distance is None else 'camera moved'}"
-                    ", per-(pixel,frame) PCG seeds)",
-            "config": {"workload": workload,
-                       "width": W, "height": H, "spp": S, "spheres": N, "bounces": B, "scene": args.scene,
-                       "parallelism": f"{world} GPU x interleaved {band_rows}-row bands",
-                       **({"gather": gather_kind} if world > 1 else {}),
-                       "rays_per_step": seg_counted},
-            "segments": {"counted_per_step": seg_counted, "traced_per_step": seg_traced,
-                         "counted_equal_every_timed_step": True,  # one counter per step, checked above
-                         "folded_per_step": seg_folded,
-                         "traced_mrays_per_s": round(seg_traced * args.steps / elapsed / 1e6, 1),
-                         "note": "every segment is counted as the reference counts it (main.cpp:390); 'folded' "
-                                 "ones belong to pixels whose every sample provably misses (dead tiles), folded "
-                                 "by the empty-tile kernel instead of traced"},
-            "cold_ms": round(cold_ms, 3),
-            "cold": {"ms": round(cold_ms, 3), "cull_pass": bool(cold_info["CullPassRan"]),
-                     "note": "first launch for this camera/scene/geometry (cull pass + untrained tile order), "
-                             "wall clock incl. its host synchronisation; the timed steps reuse the cull masks "
-                             "and the learned heaviest-first order"},
-            "roofline": roof,
-        }
+        workload = workload_name(args, W, H, S, N, B)
+        line = base_line(args, world=world, elapsed=elapsed, seg_counted=seg_counted, seg_folded=seg_folded,
+                         W=W, H=H, S=S, N=N, B=B, workload=workload,
+                         parallelism=f"{world} GPU x interleaved {band_rows}-row bands"
+                                     + (", one process per GPU (torch.distributed.run)" if world > 1 else ""),
+                         gather=gather_kind)
+        line["cold_ms"] = round(cold_ms, 3)
+        line["cold"] = {"ms": round(cold_ms, 3), "cull_pass": bool(cold_info["CullPassRan"]),
+                        "note": "first launch for this camera/scene/geometry (cull pass + untrained tile order), "
+                                "wall clock incl. its host synchronisation; the timed steps reuse the cull masks "
+                                "and the learned heaviest-first order"}
+        line["roofline"] = roofline(args, info, kern_ms, rays_local, rows[0], W, N, workload, world)
+        if world > 1:
+            line["kernel_ms_max_over_ranks"] = round(kern_ms_max, 3)
+        if one_ms is not None and world > 1:
+            line["one_gpu"] = {"ms_per_frame": round(one_ms, 3),
+                               "speedup_vs_one_gpu": round(one_ms / (elapsed / args.steps * 1e3), 3),
+                               "note": "the same frame traced whole on rank 0's GPU alone, in this run"}
         stats = dev.debug_stats()
         if stats:
             line["sched_stats"] = stats

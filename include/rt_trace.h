@@ -205,17 +205,21 @@ uint32_t rt_band_local_rows(uint32_t height, uint32_t band_rows, uint32_t band_c
  * cam->PreviousImage.Data are DEVICE pointers to compact band-local images
  * (rt_band_local_rows x Width).  `d_rays` (device u64) is incremented by
  * the bounce segments traced (RaysCastInThread, main.cpp:390).
- * Asynchronous on `stream` (hipStream_t; NULL = the HIP null stream), except
- * that the first launch for a new camera / scene / geometry on this device
- * runs the primary-ray cull pass and waits for its live-tile count (one
- * stream synchronisation); later launches with the same key reuse it.
- * Launches of one device must be issued on one stream, or the device
- * synchronises the old stream when it changes. */
+ * Asynchronous on `stream` (hipStream_t; NULL = the HIP null stream): the
+ * host never waits.  The first launch for a new camera / scene / geometry on
+ * this device runs the primary-ray cull pass; its live-tile count stays on
+ * the device (the trace grid covers every tile and blocks past the count
+ * exit) until it has reached the host asynchronously, after which launches
+ * of the same key size their grids exactly.  When the stream changes between
+ * launches, the new stream waits (device-side) for the old one's last trace.
+ * (Buffer growth for a larger geometry than any before is the one host wait.) */
 int rt_trace(rt_device *dev, const rt_camera_info *cam, const rt_trace_desc *desc,
              uint64_t *d_rays, void *stream);
 
-/* What the last rt_trace on `dev` launched (host-side bookkeeping, no GPU
- * synchronisation).  The reference counts every bounce segment, misses
+/* What the last rt_trace on `dev` launched.  Host-side bookkeeping, except
+ * that TilesTraced and SegmentsFolded need the cull pass's totals: when the
+ * last launch's key is new and they have not reached the host yet, this call
+ * waits for them (the only blocking part).  The reference counts every bounce segment, misses
  * included (RaysCastInThread, main.cpp:390); segments of pixels whose every
  * sample provably misses (no primary ray of their tile can reach a sphere,
  * no sky term) are counted analytically and folded by a pixel kernel rather
@@ -295,8 +299,13 @@ int rt_multi_scene_upload(rt_multi *m, const rt_scene *scene);
  *                            desc->BandCount / BandIndex must be 0.
  *   d_rays                 : DEVICE u64 on devices[0], incremented by the
  *                            segments every device traced.
- * Ordered after prior work on `stream` (a stream of devices[0]; NULL = the
- * null stream); work enqueued on `stream` afterwards sees the gathered frame. */
+ * Everything the caller sees (frame, mean, d_rays) is written after prior
+ * work on `stream` (a stream of devices[0]; NULL = the null stream), and work
+ * enqueued on `stream` afterwards sees the gathered frame.  The traces read
+ * nothing of the caller's and do not wait for that prior work: each device
+ * alternates between two band-image slots, so call k's gather overlaps call
+ * k+1's traces.  A continuation's PreviousRayCount must equal the frames the
+ * resident means hold (RT_EINVAL otherwise); a failed call drops them. */
 int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
                    void *stream);
 int rt_multi_synchronize(rt_multi *m);
@@ -306,9 +315,15 @@ typedef struct rt_multi_info {
     uint32_t Transport;      /* RT_MULTI_RCCL or RT_MULTI_PEER */
     uint32_t BandRows;       /* of the last trace */
     uint32_t MaxLocalRows;   /* rows of the largest device share */
-    uint64_t SegmentsFolded; /* dead-tile segments counted, not traced (last trace, all devices) */
+    uint64_t SegmentsFolded; /* dead-tile segments counted, not traced (last trace, all devices;
+                                may wait for each device's cull totals, as rt_trace_last_info) */
 } rt_multi_info;
 int rt_multi_get_info(rt_multi *m, rt_multi_info *out);
+
+/* Each device's trace time (ms, HIP events around its rt_trace on its own
+ * stream) of the last rt_multi_trace call, devices[i] -> ms_out[i]; count >=
+ * the device count.  Waits for those traces to finish. */
+int rt_multi_last_trace_ms(rt_multi *m, float *ms_out, uint32_t count);
 
 /* ----------------------------------- several GPUs, one process per GPU (RCCL) */
 
@@ -417,6 +432,22 @@ int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
  * (WorkQueueWaitUntilCompletion, base.h:175). */
 int rt_on_render_wait(void);
 int rt_on_shutdown(void);
+
+/* Where rt_on_render's time goes (cumulative since init or the last reset).
+ * Each frame's RGBA8 image and ray count are copied to pinned host memory by
+ * the frame's own stream work (a GPU-side DMA after the trace), so handing a
+ * completed frame out is a host copy (the reference's CopyImage,
+ * main.cpp:688-697) and needs no GPU round trip. */
+typedef struct rt_on_render_profile {
+    uint64_t Calls;          /* rt_on_render calls                                   */
+    uint64_t FramesLaunched; /* frames started (trace + its copies to the host)      */
+    uint64_t FramesCopied;   /* completed frames handed to the caller's image        */
+    double CallMs;           /* host time inside rt_on_render                         */
+    double HostCopyMs;       /* of which: pinned frame -> caller image (CopyImage)    */
+    double HostWaitMs;       /* of which: waiting for an in-flight frame (reset/move) */
+    double GpuFrameMs;       /* sum of completed frames' launch -> done GPU time      */
+} rt_on_render_profile;
+int rt_on_render_get_profile(rt_on_render_profile *out, int reset);
 
 /* ----------------------------------------------------------- output path */
 

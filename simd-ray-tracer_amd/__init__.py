@@ -99,6 +99,11 @@ class RtMultiInfo(ctypes.Structure):  # rt_multi_get_info
         ("SegmentsFolded", c_uint64)]
 
 
+class RtOnRenderProfile(ctypes.Structure):  # rt_on_render_get_profile
+    _fields_ = [(n, c_uint64) for n in ("Calls", "FramesLaunched", "FramesCopied")] + [
+        (n, c_double) for n in ("CallMs", "HostCopyMs", "HostWaitMs", "GpuFrameMs")]
+
+
 RT_MULTI_AUTO, RT_MULTI_RCCL, RT_MULTI_PEER = 0, 1, 2
 RT_COMM_ID_BYTES = 128
 
@@ -133,6 +138,7 @@ SIGNATURES = {
     "rt_multi_trace": (c_int, [c_void_p, POINTER(RtCameraInfo), POINTER(RtTraceDesc), c_void_p, c_void_p]),
     "rt_multi_synchronize": (c_int, [c_void_p]),
     "rt_multi_get_info": (c_int, [c_void_p, POINTER(RtMultiInfo)]),
+    "rt_multi_last_trace_ms": (c_int, [c_void_p, c_void_p, c_uint32]),
     "rt_comm_unique_id": (c_int, [c_void_p]),
     "rt_comm_create": (c_int, [c_int, c_void_p, c_uint32, c_uint32, POINTER(c_void_p)]),
     "rt_comm_destroy": (c_int, [c_void_p]),
@@ -151,6 +157,7 @@ SIGNATURES = {
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
     "rt_on_render_wait": (c_int, []),
     "rt_on_shutdown": (c_int, []),
+    "rt_on_render_get_profile": (c_int, [POINTER(RtOnRenderProfile), c_int]),
     "rt_image_write_ppm": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
     "rt_image_write_png": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
 }
@@ -288,7 +295,9 @@ def scene_clusters(scene: RtScene, simd: bool = True):
     if nf4.value:
         _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), tab.ctypes.data, nf4.value, ctypes.byref(nf4),
                                        ctypes.byref(ncp)), "rt_scene_clusters")
-    groups = (scene.ScalarSpheres.Count + 3) // 4
+    # the pair-mask words follow the rule set's group count (rt_host.cpp pack_set):
+    # SIMDSpheres groups for the SIMD rules, ceil(ScalarSpheres / 4) for the scalar ones
+    groups = scene.SIMDSpheres.Count if simd else (scene.ScalarSpheres.Count + 3) // 4
     words = 1 if groups <= 32 else 2 if groups <= 64 else 4
     return tab.reshape(-1, 4 if words == 1 else 3 + words, 4), int(ncp.value)
 
@@ -411,6 +420,12 @@ class Multi:
         _check(lib().rt_multi_trace(self.handle, ctypes.byref(c), ctypes.byref(d), c_void_p(rays_ptr),
                                     c_void_p(stream or 0)), "rt_multi_trace")
 
+    def last_trace_ms(self, n_devices: int) -> list:
+        """Each device's trace time (ms) of the last trace call (waits for them)."""
+        out = (c_float * n_devices)()
+        _check(lib().rt_multi_last_trace_ms(self.handle, out, n_devices), "rt_multi_last_trace_ms")
+        return [float(v) for v in out]
+
     def info(self) -> dict:
         i = RtMultiInfo()
         _check(lib().rt_multi_get_info(self.handle, ctypes.byref(i)), "rt_multi_get_info")
@@ -510,6 +525,15 @@ def on_render_wait() -> None:
 
 def on_shutdown() -> None:
     _check(lib().rt_on_shutdown(), "rt_on_shutdown")
+
+
+def on_render_profile(reset: bool = False) -> dict:
+    """Where rt_on_render's time went (rt_on_render_get_profile): calls, frames
+    launched / handed out, host ms in the call, its frame copies and waits,
+    and the frames' GPU time."""
+    p = RtOnRenderProfile()
+    _check(lib().rt_on_render_get_profile(ctypes.byref(p), int(reset)), "rt_on_render_get_profile")
+    return {n: (int(getattr(p, n)) if t is c_uint64 else float(getattr(p, n))) for n, t in RtOnRenderProfile._fields_}
 
 
 # ------------------------------------------------------------ output path

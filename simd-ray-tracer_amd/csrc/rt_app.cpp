@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
 #include <string.h>
+#include <time.h>
 
 #include "rt_trace.h"
 
@@ -72,28 +73,55 @@ struct App {
     uint32_t width = 0, height = 0;
     void *d_prev = nullptr, *d_cur = nullptr;
     uint64_t *d_rays = nullptr;
+    // Each launched frame is followed on the stream by asynchronous copies of
+    // its RGBA8 image and ray count into pinned host memory, so a completed
+    // frame is already on the host: handing it out is the reference's
+    // CopyImage (main.cpp:688-697), a host copy, with no GPU round trip.
+    uint32_t *h_frame = nullptr;  // pinned, width x height
+    uint64_t *h_rays = nullptr;   // pinned
+    bool h_valid = false;         // h_frame / h_rays hold the last launched frame (once complete)
     hipEvent_t ev_start = nullptr, ev_done = nullptr;
     hipStream_t stream = nullptr;
     bool in_flight = false;
     rt_camera_info cam;
+    rt_on_render_profile prof;
 };
 App g_app;
 
+double now_ms() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
 bool frame_complete() {
     if (!g_app.in_flight) return true;
-    return hipEventQuery(g_app.ev_done) == hipSuccess;
+    if (hipEventQuery(g_app.ev_done) == hipSuccess) return true;
+    (void)hipGetLastError();  // "not ready" must not reach a later launch check
+    return false;
 }
 
 int wait_frame() {
     if (!g_app.in_flight) return RT_OK;
+    const double t = now_ms();
     if (hipEventSynchronize(g_app.ev_done) != hipSuccess) return RT_EIO;
+    g_app.prof.HostWaitMs += now_ms() - t;
     return RT_OK;
 }
 
+// The completed frame into the caller's image: CopyImage of main.cpp:688-697
+// from the pinned copy the frame's own stream work already made.
 int copy_current(const rt_image *image) {
-    if (!g_app.d_cur || !image->Data) return RT_OK;
+    if (!image->Data) return RT_OK;
     const size_t bytes = (size_t)g_app.width * g_app.height * 4u;
-    return hipMemcpy(image->Data, g_app.d_cur, bytes, hipMemcpyDeviceToHost) == hipSuccess ? RT_OK : RT_EIO;
+    const double t = now_ms();
+    if (g_app.h_valid)
+        memcpy(image->Data, g_app.h_frame, bytes);
+    else
+        memset(image->Data, 0, bytes);  // nothing traced yet: the zero-filled CurrentImage
+    g_app.prof.HostCopyMs += now_ms() - t;
+    g_app.prof.FramesCopied += 1;
+    return RT_OK;
 }
 
 }  // namespace
@@ -131,6 +159,7 @@ extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices
     g_app.ordinal = hip_devices[0];
     if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
     if (hipMalloc(&g_app.d_rays, sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc(&g_app.h_rays, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&g_app.ev_start) != hipSuccess || hipEventCreate(&g_app.ev_done) != hipSuccess ||
         hipStreamCreateWithFlags(&g_app.stream, hipStreamNonBlocking) != hipSuccess)
         return RT_ENOMEM;
@@ -139,8 +168,20 @@ extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices
     return RT_OK;
 }
 
+static int on_render(const rt_image *image, rt_render_params params, uint32_t keys, uint64_t *out_total_rays_cast,
+                     double *out_time_elapsed_ms);
+
 extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
                             uint64_t *out_total_rays_cast, double *out_time_elapsed_ms) {
+    const double t = now_ms();
+    const int rc = on_render(image, params, keys, out_total_rays_cast, out_time_elapsed_ms);
+    g_app.prof.Calls += 1;
+    g_app.prof.CallMs += now_ms() - t;
+    return rc;
+}
+
+static int on_render(const rt_image *image, rt_render_params params, uint32_t keys, uint64_t *out_total_rays_cast,
+                     double *out_time_elapsed_ms) {
     if (!g_app.ready || !image || image->Width == 0 || image->Height == 0) return RT_EINVAL;
     if (params.SceneIndex > 2) return RT_EINVAL;
     if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
@@ -185,8 +226,12 @@ extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint
         if (resize) {
             (void)hipFree(g_app.d_prev);
             (void)hipFree(g_app.d_cur);
+            if (g_app.h_frame) (void)hipHostFree(g_app.h_frame);
             g_app.d_prev = g_app.d_cur = nullptr;
-            if (hipMalloc(&g_app.d_prev, px * 16u) != hipSuccess || hipMalloc(&g_app.d_cur, px * 4u) != hipSuccess)
+            g_app.h_frame = nullptr;
+            g_app.h_valid = false;
+            if (hipMalloc(&g_app.d_prev, px * 16u) != hipSuccess || hipMalloc(&g_app.d_cur, px * 4u) != hipSuccess ||
+                hipHostMalloc(&g_app.h_frame, px * 4u, hipHostMallocDefault) != hipSuccess)
                 return RT_ENOMEM;
             g_app.width = image->Width;
             g_app.height = image->Height;
@@ -212,14 +257,15 @@ extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint
     g_app.cam.PreviousImage.Width = g_app.width;
     g_app.cam.PreviousImage.Height = g_app.height;
     g_app.cam.PreviousImage.Format = RT_FORMAT_R32B32G32A32_F32;
-    if (copy_out && out_total_rays_cast) {  // :840-842
-        if (hipMemcpy(out_total_rays_cast, g_app.d_rays, sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
-            return RT_EIO;
-    }
-    if (out_time_elapsed_ms) {  // :848
+    if (copy_out && out_total_rays_cast) *out_total_rays_cast = g_app.h_valid ? *g_app.h_rays : 0u;  // :840-842
+    {  // :848 (the previous frame has completed here: on every path above)
         float ms = 0.0f;
-        if (g_app.in_flight && hipEventElapsedTime(&ms, g_app.ev_start, g_app.ev_done) != hipSuccess) ms = 0.0f;
-        *out_time_elapsed_ms = ms;
+        if (g_app.in_flight && hipEventElapsedTime(&ms, g_app.ev_start, g_app.ev_done) != hipSuccess) {
+            (void)hipGetLastError();
+            ms = 0.0f;
+        }
+        g_app.prof.GpuFrameMs += ms;
+        if (out_time_elapsed_ms) *out_time_elapsed_ms = ms;
     }
     if (hipMemsetAsync(g_app.d_rays, 0, sizeof(uint64_t), g_app.stream) != hipSuccess) return RT_EIO;  // :843-846
     rt_trace_desc desc;
@@ -243,9 +289,23 @@ extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint
         rc = rt_trace(g_app.dev, &g_app.cam, &desc, g_app.d_rays, g_app.stream);
     }
     if (rc) return rc;
+    // the frame's image and count follow it to the host (the next call hands them out)
+    if (hipMemcpyAsync(g_app.h_frame, g_app.d_cur, (size_t)g_app.width * g_app.height * 4u, hipMemcpyDeviceToHost,
+                       g_app.stream) != hipSuccess ||
+        hipMemcpyAsync(g_app.h_rays, g_app.d_rays, sizeof(uint64_t), hipMemcpyDeviceToHost, g_app.stream) != hipSuccess)
+        return RT_EIO;
     if (hipEventRecord(g_app.ev_done, g_app.stream) != hipSuccess) return RT_EIO;
+    g_app.h_valid = true;
     g_app.in_flight = true;
+    g_app.prof.FramesLaunched += 1;
     return copy_out ? 1 : 0;
+}
+
+extern "C" int rt_on_render_get_profile(rt_on_render_profile *out, int reset) {
+    if (!out) return RT_EINVAL;
+    *out = g_app.prof;
+    if (reset) g_app.prof = rt_on_render_profile{};
+    return RT_OK;
 }
 
 extern "C" int rt_on_render_wait(void) { return g_app.ready ? wait_frame() : RT_OK; }
@@ -256,6 +316,8 @@ extern "C" int rt_on_shutdown(void) {
     (void)hipFree(g_app.d_prev);
     (void)hipFree(g_app.d_cur);
     (void)hipFree(g_app.d_rays);
+    if (g_app.h_frame) (void)hipHostFree(g_app.h_frame);
+    if (g_app.h_rays) (void)hipHostFree(g_app.h_rays);
     (void)hipEventDestroy(g_app.ev_start);
     (void)hipEventDestroy(g_app.ev_done);
     (void)hipStreamDestroy(g_app.stream);

@@ -61,18 +61,32 @@ struct rt_device {
     uint32_t order_launches = 6;      // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept
     uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
     uint32_t *d_tile_live = nullptr;
-    unsigned long long *d_cull_counters = nullptr;  // 2 x 64 striped counters of the cull pass
+    unsigned long long *d_cull_counters = nullptr;  // kCullCounterWords: striped counters + device totals of the cull pass
     uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
     size_t tile_cap = 0, mask_cap = 0;
     size_t mask_words = 0;  // words the last cull pass wrote (rt_debug_masks)
     // the launch (camera, scene, geometry) the masks / live list / order were made for
     std::vector<uint32_t> tile_key;
     bool tile_order_valid = false;
+    // The cull pass's totals travel to the host asynchronously (pinned h_counts,
+    // event ev_counts): a new key never blocks the host.  Until they have
+    // landed (counts_known), launches size their grids for every tile and read
+    // the live count on the device (TraceArgs.live_total).
     uint32_t n_live = 0;
     uint64_t dead_pixels = 0;
+    bool counts_known = true;
+    unsigned long long *h_counts = nullptr;  // pinned {live tiles, dead pixels}
+    hipEvent_t ev_counts = nullptr;
     uint64_t scene_gen = 0;  // bumped by every rt_scene_upload
+    // the last stream rt_trace ran on, and an event (owned here) after its last
+    // launch: uploads, buffer growth, stream switches and destroy wait on it
     hipStream_t tile_stream = nullptr;
     bool tile_stream_set = false;
+    hipEvent_t ev_traced = nullptr;
+    bool traced_recorded = false;
+    // what rt_trace_last_info resolves lazily (the folded segments need the counts)
+    uint32_t last_n_tiles = 0, last_frames = 0;
+    bool last_empty_capable = false;
     uint32_t cu_count = 256;
     unsigned long long *d_stats = nullptr;  // RT_STATS=1: per-launch scheduling counters
     unsigned long long *d_wave_times = nullptr;  // RT_WAVETIMES=1: per-wave start/end of the last launch
@@ -123,9 +137,12 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     rt_device *d = new rt_device();
     d->ordinal = hip_device;
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->d_lut, 2048 * sizeof(float)) != hipSuccess) {
-        delete d;
-        return fail(RT_ENOMEM, "rt_device_create: stream/LUT allocation failed");
+        hipMalloc(&d->d_lut, 2048 * sizeof(float)) != hipSuccess ||
+        hipHostMalloc(&d->h_counts, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_counts, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_traced, hipEventDisableTiming) != hipSuccess) {
+        rt_device_destroy(d);
+        return fail(RT_ENOMEM, "rt_device_create: stream/LUT/event allocation failed");
     }
     {
         hipDeviceProp_t prop;
@@ -183,7 +200,9 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
 extern "C" int rt_device_destroy(rt_device *d) {
     if (!d) return RT_OK;
     (void)hipSetDevice(d->ordinal);
-    (void)hipStreamSynchronize(d->stream);
+    // the caller's trace stream may already be gone: wait on the owned event
+    if (d->traced_recorded) (void)hipEventSynchronize(d->ev_traced);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (int r = 0; r < 2; ++r) {
         (void)hipFree(d->d_groups[r]);
         (void)hipFree(d->d_mats[r]);
@@ -192,26 +211,49 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_lut);
     (void)hipFree(d->d_stats);
     (void)hipFree(d->d_wave_times);
-    if (d->tile_stream_set) (void)hipStreamSynchronize(d->tile_stream);
     (void)hipFree(d->d_tile_cost);
     (void)hipFree(d->d_tile_order);
     (void)hipFree(d->d_tile_scratch);
     (void)hipFree(d->d_tile_live);
     (void)hipFree(d->d_cull_counters);
     (void)hipFree(d->d_masks);
-    (void)hipStreamDestroy(d->stream);
+    if (d->h_counts) (void)hipHostFree(d->h_counts);
+    if (d->ev_counts) (void)hipEventDestroy(d->ev_counts);
+    if (d->ev_traced) (void)hipEventDestroy(d->ev_traced);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
     return RT_OK;
 }
 
-// rt_trace is asynchronous on the caller's stream (d->tile_stream), while
-// uploads go through the device's own non-blocking stream: before a buffer a
-// trace may still read (scene groups, materials, cluster table, rsqrt table)
-// is overwritten, every launch issued so far must have finished.
+// rt_trace is asynchronous on the caller's stream, while uploads go through
+// the device's own non-blocking stream: before a buffer a trace may still
+// read (scene groups, materials, cluster table, rsqrt table) is overwritten,
+// every launch issued so far must have finished.  The wait is on the event
+// recorded after the last trace (owned by the device), not on the caller's
+// stream, which the caller may have destroyed since.
 static int quiesce(rt_device *d) {
-    if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(d->tile_stream));
+    if (d->traced_recorded) HIP_OK(hipEventSynchronize(d->ev_traced));
     HIP_OK(hipStreamSynchronize(d->stream));
     return RT_OK;
+}
+
+// Brings the cull pass's totals to the host once they have landed (wait:
+// block until they have).  Returns whether they are known.
+static bool resolve_counts(rt_device *d, bool wait) {
+    if (d->counts_known) return true;
+    if (wait) {
+        if (hipEventSynchronize(d->ev_counts) != hipSuccess) return false;
+    } else {
+        const hipError_t q = hipEventQuery(d->ev_counts);
+        if (q != hipSuccess) {
+            (void)hipGetLastError();  // "not ready" must not reach a later launch check
+            return false;
+        }
+    }
+    d->n_live = (uint32_t)d->h_counts[0];
+    d->dead_pixels = d->h_counts[1];
+    d->counts_known = true;
+    return true;
 }
 
 extern "C" int rt_set_rsqrt_table(rt_device *d, const float table[2048]) {
@@ -861,11 +903,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         key.push_back(u);
     }
     if (!d->tile_stream_set || s != d->tile_stream) {
-        // order and masks are written and read in stream order
-        if (d->tile_stream_set) HIP_OK(hipStreamSynchronize(d->tile_stream));
+        // order, masks and costs are written and read in stream order: a new
+        // stream follows every launch issued on the previous one (device-side wait)
+        if (d->traced_recorded) HIP_OK(hipStreamWaitEvent(s, d->ev_traced, 0));
         d->tile_stream = s;
         d->tile_stream_set = true;
-        d->tile_key.clear();
     }
     if (n_tiles > d->tile_cap) {
         HIP_OK(hipStreamSynchronize(s));
@@ -878,7 +920,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(n_tiles)) != hipSuccess)
             return fail(RT_ENOMEM, "rt_trace: tile order buffers");
-        if (!d->d_cull_counters && hipMalloc(&d->d_cull_counters, 128u * 8u) != hipSuccess)
+        if (!d->d_cull_counters && hipMalloc(&d->d_cull_counters, kCullCounterWords * 8u) != hipSuccess)
             return fail(RT_ENOMEM, "rt_trace: tile order buffers");
         d->tile_cap = n_tiles;
         d->tile_key.clear();
@@ -905,15 +947,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
                     0 ||
                 rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
                 return fail(RT_EIO, "rt_trace: cull pass launch failed: %s", hipGetErrorString(hipGetLastError()));
-            unsigned long long c[128];
-            HIP_OK(hipMemcpyAsync(c, d->d_cull_counters, sizeof(c), hipMemcpyDeviceToHost, s));
-            HIP_OK(hipStreamSynchronize(s));
-            d->n_live = 0;
-            d->dead_pixels = 0;
-            for (int i = 0; i < 64; ++i) {
-                d->n_live += (uint32_t)c[i];
-                d->dead_pixels += c[64 + i];
-            }
+            // the totals follow asynchronously (resolve_counts); no host wait here
+            HIP_OK(hipMemcpyAsync(d->h_counts, d->d_cull_counters + kCullTotals, 2 * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, s));
+            HIP_OK(hipEventRecord(d->ev_counts, s));
+            d->counts_known = false;
             d->tile_order_valid = true;
             // The first launch of a key has no measured tile costs, and in the cull
             // pass's live-first order its heavy tiles start late and form the tail
@@ -924,7 +962,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             // changes no bit: the owner lane folds frames in order either way, and
             // frame k's seed and weights depend on PreviousRayCount + k only.
             const uint32_t split_min = 4u * d->head_samples * (uint32_t)lpp;
-            if (sched && d->split_env && d->n_live > 0 && desc->Frames >= split_min) {
+            if (sched && d->split_env && desc->Frames >= split_min) {
                 // leading parts of head_samples, x split_growth, ... samples per lane
                 // while the rest keeps at least half the frames
                 uint32_t f = d->head_samples * (uint32_t)lpp, used = 0;
@@ -939,16 +977,25 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_tiles * 4u, s));
             d->n_live = n_tiles;
             d->dead_pixels = 0;
+            d->counts_known = true;
             d->tile_order_valid = false;  // identity until a measured sort exists
         }
     }
+    // live-tile count: on the host once the cull totals have landed, else read
+    // by the kernels from the device (grid over every tile, early exit)
+    const bool known = resolve_counts(d, false);
+    const uint32_t grid_tiles = known ? d->n_live : n_tiles;
+    a.live_total = known ? nullptr : d->d_cull_counters + kCullTotals;
+    const bool any_live = !known || d->n_live > 0;
+    const bool any_dead = empty_capable && (!known || d->n_live < n_tiles);
     a.masks = cull ? d->d_masks : nullptr;
     a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
     a.tile_cost = sched ? d->d_tile_cost : nullptr;
-    d->last.SegmentsFolded = empty_capable && d->n_live < n_tiles ? d->dead_pixels * desc->Frames : 0u;
+    d->last_n_tiles = n_tiles;
+    d->last_frames = desc->Frames;
+    d->last_empty_capable = empty_capable;
     d->last.LanesPerPixel = (uint32_t)lpp;
     d->last.TilesTotal = n_tiles;
-    d->last.TilesTraced = d->n_live;
     d->last.CullPassRan = cull && new_key ? 1u : 0u;
     d->last.OrderedLaunches = d->n_sorts;
     d->last.ClusteredWalk = a.clusters ? 1u : 0u;
@@ -967,16 +1014,15 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         }
         a.frames = split[part];
         done_frames += split[part];
-        if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, d->n_live, s) != 0)
+        if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, grid_tiles, s) != 0)
             return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
-        if (empty_capable && d->n_live < n_tiles &&
-            rtk_launch_empty(&a, lpp, d->d_tile_live, (unsigned long long)(d->dead_pixels * a.frames), s) != 0)
+        if (any_dead && rtk_launch_empty(&a, lpp, d->d_tile_live, d->d_cull_counters + kCullTotals + 1, s) != 0)
             return fail(RT_EIO, "rt_trace: empty-tile launch failed: %s", hipGetErrorString(hipGetLastError()));
         // the learned order settles within a few launches (C2: 7.7, 6.3, 6.1, 5.9,
         // 5.8 ms); after order_launches re-sorts (RT_ORDER_LAUNCHES, default 6)
         // the order is kept and the three sort kernels (~14 us per launch, 1.5 %
         // of an 8-rank C2 share) are skipped
-        if (sched && d->n_live > 0 && (d->n_sorts < d->order_launches || part + 1 < n_split)) {
+        if (sched && any_live && (d->n_sorts < d->order_launches || part + 1 < n_split)) {
             d->n_sorts += 1;
             if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
                 return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
@@ -984,6 +1030,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         }
     }
     d->last.SplitHeadFrames = head_frames;
+    HIP_OK(hipEventRecord(d->ev_traced, s));
+    d->traced_recorded = true;
     return RT_OK;
 }
 
@@ -1012,6 +1060,14 @@ extern "C" int rt_encode_rgba8(const float *d_accum_v4, uint32_t *d_rgba8, uint6
 
 extern "C" int rt_trace_last_info(rt_device *d, rt_trace_info *out) {
     if (!d || !out) return fail(RT_EINVAL, "rt_trace_last_info: NULL argument");
+    // the live/dead totals of the last launch's key: waits for them if they
+    // are still on their way from the device (the only blocking part)
+    HIP_OK(hipSetDevice(d->ordinal));
+    if (!resolve_counts(d, true)) return fail(RT_EIO, "rt_trace_last_info: cull totals: %s",
+                                              hipGetErrorString(hipGetLastError()));
+    d->last.TilesTraced = d->n_live;
+    d->last.SegmentsFolded = d->last_empty_capable && d->n_live < d->last_n_tiles
+                                 ? d->dead_pixels * d->last_frames : 0u;
     *out = d->last;
     return RT_OK;
 }

@@ -72,7 +72,15 @@ struct TraceArgs {
     uint32_t pf_relative;        // prefilter: row 3 holds r^2 and the threshold is per lane (rt_kernel.hip kPfRel)
     uint32_t solo;               // one wave per workgroup (4 x tiles workgroups of 64 threads; needs no LDS image)
     uint32_t walk;               // kWalk*: the one-wave kernel specialised for this launch's secondary walk
+    // optional: live block tiles of the cull pass, on the device (kCullTotals).  Set while the host
+    // has not read the count back: the grid then covers every tile and blocks past the count exit.
+    const unsigned long long *live_total;
 };
+// Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)
+// striped image pixels of dead block tiles, then the two totals at kCullTotals
+// (live tiles, dead pixels), summed on the device after the pass.
+constexpr uint32_t kCullCounterWords = 132;
+constexpr uint32_t kCullTotals = 128;
 // Secondary-ray walk variants (rt_kernel.hip Walk<>): any (run-time dispatch),
 // the per-group loops, or a cluster walk with 1/2/4 pair-mask words and
 // scene-wide or per-lane ("Rel") thresholds
@@ -122,14 +130,16 @@ extern "C" int rtk_launch_trace_grid(const TraceArgs *a, int simd, int src, int 
 // per block tile live[t] (some wave tile has a candidate group, or
 // !empty_capable) and cost[t] = live ? 2 : 0 (so a tile sort puts live tiles
 // first); counters[0, 64) sum to the live tiles, counters[64, 128) to the
-// image pixels of dead tiles (zeroed by the call).
+// image pixels of dead tiles (zeroed by the call), and counters[kCullTotals],
+// counters[kCullTotals + 1] receive the two sums (kCullCounterWords words).
 extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t *live, uint32_t *cost,
                                unsigned long long *counters, int empty_capable, hipStream_t stream);
 // Pixels of dead block tiles (live[t] == 0): every sample misses with no sky,
-// so fold zeros into the running mean, store both images; adds dead_rays
-// (dead pixels x frames) to the ray counter once.
+// so fold zeros into the running mean, store both images; adds
+// dead_pixels[0] x a->frames segments to the ray counter once (dead_pixels:
+// the cull pass's device total, so the host need not read it back).
 extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
-                                unsigned long long dead_rays, hipStream_t stream);
+                                const unsigned long long *dead_pixels, hipStream_t stream);
 // dst[0] += sum of slots[0, n) (the gathered per-device ray counters)
 extern "C" int rtk_launch_sum_u64(const uint64_t *slots, uint32_t n, uint64_t *dst, hipStream_t stream);
 // sets rt_last_error()'s text and returns `code` (rt_host.cpp)

@@ -915,6 +915,9 @@ void trace_kernel(TraceArgs a) {
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
     constexpr uint32_t kRing = Ring<P>::N;
     extern __shared__ float4 smem[];
+    // first launch of a key: the host has not read the live-tile count back, so
+    // the grid covers every tile (live first) and blocks past the count leave
+    if (a.live_total && (SOLO ? blockIdx.x >> 2 : blockIdx.x) >= (uint32_t)*a.live_total) return;
     const uint64_t st_entry = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
@@ -1419,16 +1422,35 @@ __global__ __launch_bounds__(256) void cull_kernel(TraceArgs a, uint32_t *live, 
     }
 }
 
+// The cull pass's striped counters summed on the device (one wave), so no
+// launch needs the host to read them: counters[kCullTotals] = live block
+// tiles, counters[kCullTotals + 1] = image pixels of dead block tiles.
+#ifndef RTK_P16_TU
+__global__ __launch_bounds__(64) void cull_total_kernel(unsigned long long *counters) {
+    const uint32_t lane = threadIdx.x;
+    unsigned long long live = counters[lane], dead = counters[kCullStripes + lane];
+    for (int off = 32; off > 0; off >>= 1) {
+        live += __shfl_xor(live, off);
+        dead += __shfl_xor(dead, off);
+    }
+    if (lane == 0) {
+        counters[kCullTotals] = live;
+        counters[kCullTotals + 1] = dead;
+    }
+}
+#endif
+
 // Pixels of dead block tiles: no sphere group passes any of the tile's
 // (conservative) cone tests, so every primary ray of every sample misses;
 // without a sky term each sample's Out is exactly 0 (main.cpp:433-440), its
-// one segment still counts (main.cpp:390; dead_rays = dead pixels x frames
-// from the cull pass, added once), and its blend is
+// one segment still counts (main.cpp:390; dead pixels x frames, the pixels
+// from the cull pass's device total, added once), and its blend is
 // Final = 0*(1/n) + Prev*((n-1)/n) = RN(Prev*((n-1)/n)) -- folded here without
 // generating the rays (an all-zero running mean stays exactly zero).  The
 // ratios are the trace kernel's fold-table values.
 template <int P>
-__global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t *live, unsigned long long dead_rays) {
+__global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t *live,
+                                                    const unsigned long long *dead_pixels) {
     constexpr uint32_t BW = 2u * Shape<P>::TW, BH = 2u * Shape<P>::TH;
     __shared__ float ratio[kFoldTable];
     const bool fold = a.prev_count > 0 && !(a.flags & kFlagAccumZero);
@@ -1438,7 +1460,10 @@ __global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t 
             ratio[i] = (float)pc / (float)(pc + 1u);
         }
     __syncthreads();
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && dead_rays) atomicAdd(a.rays, dead_rays);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        const unsigned long long dead_rays = *dead_pixels * a.frames;
+        if (dead_rays) atomicAdd(a.rays, dead_rays);
+    }
     const uint32_t x = blockIdx.x * 256u + threadIdx.x, ly = blockIdx.y;
     if (!(x < a.width && live[(ly / BH) * a.tiles_x + x / BW] == 0u)) return;
     const size_t pix = (size_t)ly * a.width + x;
@@ -1760,6 +1785,7 @@ static void launch_cull_p(const TraceArgs *a, uint32_t *live, uint32_t *cost, un
     (void)hipMemsetAsync(counters, 0, 2u * rtk::kCullStripes * sizeof(unsigned long long), stream);
     hipLaunchKernelGGL(rtk::cull_kernel<P>, dim3(n), dim3(256), 0, stream, *a, live, cost, counters,
                        (uint32_t)(empty_capable != 0));
+    hipLaunchKernelGGL(rtk::cull_total_kernel, dim3(1), dim3(64), 0, stream, counters);
 }
 
 extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t *live, uint32_t *cost,
@@ -1770,15 +1796,15 @@ extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t
 }
 
 template <int P>
-static void launch_empty_p(const TraceArgs *a, const uint32_t *live, unsigned long long dead_rays,
+static void launch_empty_p(const TraceArgs *a, const uint32_t *live, const unsigned long long *dead_pixels,
                            hipStream_t stream) {
     hipLaunchKernelGGL(rtk::empty_kernel<P>, dim3((a->width + 255u) / 256u, a->local_rows), dim3(256), 0, stream, *a,
-                       live, dead_rays);
+                       live, dead_pixels);
 }
 
 extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
-                                unsigned long long dead_rays, hipStream_t stream) {
-    RTK_BY_P(launch_empty_p, a, live, dead_rays, stream)
+                                const unsigned long long *dead_pixels, hipStream_t stream) {
+    RTK_BY_P(launch_empty_p, a, live, dead_pixels, stream)
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 #undef RTK_BY_P

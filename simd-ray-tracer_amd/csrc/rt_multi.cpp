@@ -99,15 +99,25 @@ int grow(T **p, size_t *cap, size_t bytes) {  // device allocation on the curren
     return RT_OK;
 }
 
+// Calls alternate between two slots of every shard's band image and ray
+// counter, so call k's gather (reading slot k & 1) overlaps call k+1's trace
+// (writing the other slot); a slot is traced again only after the gather two
+// calls back has read it.
+constexpr int kSlots = 2;
+
 struct Shard {
     int ordinal = 0;
     rt_device *dev = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t traced = nullptr;  // this device's trace of the current call is done
-    float4 *prev = nullptr;       // resident running mean of this device's bands
-    uint32_t *cur = nullptr;      // RGBA8 of this device's bands
-    uint64_t *rays = nullptr;     // segments this device traced in the current call
+    hipStream_t stream = nullptr;      // traces
+    hipStream_t xfer = nullptr;        // RCCL sends of this device's images (off the trace stream)
+    hipEvent_t traced[kSlots] = {};    // the trace into slot b is done
+    hipEvent_t sent[kSlots] = {};      // RCCL: the sends of slot b are done (slot b free again)
+    hipEvent_t t0[kSlots] = {}, t1[kSlots] = {};  // timing of the trace into slot b
+    float4 *prev = nullptr;            // resident running mean of this device's bands
+    uint32_t *cur[kSlots] = {};        // RGBA8 of this device's bands
+    uint64_t *rays[kSlots] = {};       // segments this device traced into slot b
     size_t cap_prev = 0, cap_cur = 0;
+    bool launched = false;             // the last call launched a trace here (rows > 0, frames > 0)
     ncclComm_t comm = nullptr;
 };
 
@@ -116,32 +126,39 @@ struct Shard {
 struct rt_multi {
     std::vector<Shard> s;
     uint32_t transport = RT_MULTI_PEER;
-    // devices[0]: staging for the gathered compact images, the gathered ray
-    // counters, and the event the next call's traces wait on (the staging
-    // and the shards' images are reused by the next call)
+    // devices[0]: staging for the gathered compact images and ray counters
     uint8_t *stage_cur = nullptr, *stage_prev = nullptr;
     size_t cap_stage_cur = 0, cap_stage_prev = 0;
     uint64_t *ray_slots = nullptr;
     hipStream_t gather = nullptr;  // devices[0]
     hipEvent_t start = nullptr, gathered = nullptr;
-    bool gathered_valid = false;
-    // geometry the resident running means belong to
+    hipEvent_t copied[kSlots] = {};   // peer transport: slot b's copies are done (slot b free again)
+    bool slot_used[kSlots] = {};      // slot b has been gathered before (its free event is valid)
+    uint32_t calls = 0;               // rt_multi_trace calls (slot = calls & 1)
+    bool prev_gathered = false;       // the last call also gathered the resident running means
+    // geometry the resident running means belong to, and the frames folded there
     uint32_t width = 0, height = 0, band_rows = 0;
     bool accum_valid = false;
-    uint32_t last_band_rows = 0, last_max_rows = 0;
-    uint64_t last_folded = 0;
+    uint64_t resident_frames = 0;
+    uint32_t last_band_rows = 0, last_max_rows = 0, last_slot = 0;
 };
 
 static void destroy_shard(Shard &sh) {
     (void)hipSetDevice(sh.ordinal);
     if (sh.stream) (void)hipStreamSynchronize(sh.stream);
+    if (sh.xfer) (void)hipStreamSynchronize(sh.xfer);
+    // the device first: it waits on its own event after the last trace, issued on sh.stream
+    if (sh.dev) rt_device_destroy(sh.dev);
     if (sh.comm && rccl().ok) (void)rccl().CommDestroy(sh.comm);
     (void)hipFree(sh.prev);
-    (void)hipFree(sh.cur);
-    (void)hipFree(sh.rays);
-    if (sh.traced) (void)hipEventDestroy(sh.traced);
+    for (int b = 0; b < kSlots; ++b) {
+        (void)hipFree(sh.cur[b]);
+        (void)hipFree(sh.rays[b]);
+        for (hipEvent_t e : {sh.traced[b], sh.sent[b], sh.t0[b], sh.t1[b]})
+            if (e) (void)hipEventDestroy(e);
+    }
+    if (sh.xfer) (void)hipStreamDestroy(sh.xfer);
     if (sh.stream) (void)hipStreamDestroy(sh.stream);
-    if (sh.dev) rt_device_destroy(sh.dev);
     sh = Shard();
 }
 
@@ -150,6 +167,7 @@ extern "C" int rt_multi_destroy(rt_multi *m) {
     for (Shard &sh : m->s) {
         (void)hipSetDevice(sh.ordinal);
         if (sh.stream) (void)hipStreamSynchronize(sh.stream);
+        if (sh.xfer) (void)hipStreamSynchronize(sh.xfer);
     }
     if (!m->s.empty()) {
         (void)hipSetDevice(m->s[0].ordinal);
@@ -157,8 +175,8 @@ extern "C" int rt_multi_destroy(rt_multi *m) {
         (void)hipFree(m->stage_cur);
         (void)hipFree(m->stage_prev);
         (void)hipFree(m->ray_slots);
-        if (m->start) (void)hipEventDestroy(m->start);
-        if (m->gathered) (void)hipEventDestroy(m->gathered);
+        for (hipEvent_t e : {m->start, m->gathered, m->copied[0], m->copied[1]})
+            if (e) (void)hipEventDestroy(e);
         if (m->gather) (void)hipStreamDestroy(m->gather);
     }
     for (Shard &sh : m->s) destroy_shard(sh);
@@ -181,10 +199,15 @@ extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t 
             rt_multi_destroy(m);
             return rc;
         }
-        if (hipSetDevice(sh.ordinal) != hipSuccess ||
-            hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&sh.traced, hipEventDisableTiming) != hipSuccess ||
-            hipMalloc(&sh.rays, sizeof(uint64_t)) != hipSuccess) {
+        bool ok = hipSetDevice(sh.ordinal) == hipSuccess &&
+                  hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithFlags(&sh.xfer, hipStreamNonBlocking) == hipSuccess;
+        for (int b = 0; ok && b < kSlots; ++b)
+            ok = hipEventCreateWithFlags(&sh.traced[b], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&sh.sent[b], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreate(&sh.t0[b]) == hipSuccess && hipEventCreate(&sh.t1[b]) == hipSuccess &&
+                 hipMalloc(&sh.rays[b], sizeof(uint64_t)) == hipSuccess;
+        if (!ok) {
             rt_multi_destroy(m);
             return rt_fail(RT_ENOMEM, "rt_multi_create: stream/event/counter on device %d", sh.ordinal);
         }
@@ -193,6 +216,8 @@ extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t 
     if (hipSetDevice(d0) != hipSuccess || hipStreamCreateWithFlags(&m->gather, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&m->start, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->gathered, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->copied[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->copied[1], hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&m->ray_slots, RT_MULTI_MAX_DEVICES * sizeof(uint64_t)) != hipSuccess) {
         rt_multi_destroy(m);
         return rt_fail(RT_ENOMEM, "rt_multi_create: gather resources on device %d", d0);
@@ -252,6 +277,7 @@ extern "C" int rt_multi_synchronize(rt_multi *m) {
     for (Shard &sh : m->s) {
         MHIP(hipSetDevice(sh.ordinal));
         MHIP(hipStreamSynchronize(sh.stream));
+        MHIP(hipStreamSynchronize(sh.xfer));
         if (const int rc = rt_device_synchronize(sh.dev)) return rc;
     }
     MHIP(hipSetDevice(m->s[0].ordinal));
@@ -265,16 +291,40 @@ extern "C" int rt_multi_get_info(rt_multi *m, rt_multi_info *out) {
     out->Transport = m->transport;
     out->BandRows = m->last_band_rows;
     out->MaxLocalRows = m->last_max_rows;
-    out->SegmentsFolded = m->last_folded;
+    // dead-tile segments of the last call: resolved per device (each may wait
+    // for its cull pass's totals to reach the host, rt_trace_last_info)
+    uint64_t folded = 0;
+    for (Shard &sh : m->s)
+        if (sh.launched) {
+            rt_trace_info info;
+            if (const int rc = rt_trace_last_info(sh.dev, &info)) return rc;
+            folded += info.SegmentsFolded;
+        }
+    out->SegmentsFolded = folded;
     return RT_OK;
 }
+
+extern "C" int rt_multi_last_trace_ms(rt_multi *m, float *ms_out, uint32_t count) {
+    if (!m || !ms_out || count < m->s.size()) return rt_fail(RT_EINVAL, "rt_multi_last_trace_ms: bad argument");
+    if (m->calls == 0) return rt_fail(RT_EINVAL, "rt_multi_last_trace_ms: no call yet");
+    const uint32_t b = m->last_slot;
+    for (size_t i = 0; i < m->s.size(); ++i) {
+        Shard &sh = m->s[i];
+        MHIP(hipSetDevice(sh.ordinal));
+        MHIP(hipEventSynchronize(sh.t1[b]));
+        MHIP(hipEventElapsedTime(&ms_out[i], sh.t0[b], sh.t1[b]));
+    }
+    return RT_OK;
+}
+
+static int multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
+                       hipStream_t caller, bool restart, bool same_geometry);
 
 extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
                               void *stream) {
     if (!m || !cam || !desc || !d_rays) return rt_fail(RT_EINVAL, "rt_multi_trace: NULL argument");
     if (desc->BandCount != 0 || desc->BandIndex != 0)
         return rt_fail(RT_EINVAL, "rt_multi_trace: BandCount/BandIndex must be 0 (bands are dealt over the devices)");
-    const uint32_t n = (uint32_t)m->s.size();
     const uint32_t W = desc->Width, H = desc->Height, R = desc->BandRows ? desc->BandRows : 8u;
     if (W == 0 || H == 0 || W > 65536 || H > 65536 || R % 8u)
         return rt_fail(RT_EINVAL, "rt_multi_trace: bad geometry %ux%u, BandRows %u", W, H, R);
@@ -284,9 +334,31 @@ extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_t
     if (!restart && !(same_geometry && m->accum_valid))
         return rt_fail(RT_EINVAL, "rt_multi_trace: PreviousRayCount %u but no resident running mean for this geometry",
                        desc->PreviousRayCount);
+    // the resident means hold resident_frames frames: a continuation must say so,
+    // or its weights (main.cpp:484-487) would blend the wrong way
+    if (!restart && desc->PreviousRayCount != m->resident_frames)
+        return rt_fail(RT_EINVAL, "rt_multi_trace: PreviousRayCount %u but the resident running mean holds %llu frames",
+                       desc->PreviousRayCount, (unsigned long long)m->resident_frames);
+    const int rc = multi_trace(m, cam, desc, d_rays, (hipStream_t)stream, restart, same_geometry);
+    if (rc) {  // some shards may have traced (restarting their means), others not
+        m->accum_valid = false;
+        return rc;
+    }
+    if (restart) {
+        m->accum_valid = desc->Frames > 0;
+        m->resident_frames = desc->Frames;
+    } else {
+        m->resident_frames += desc->Frames;
+    }
+    return RT_OK;
+}
+
+static int multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
+                       hipStream_t caller, bool restart, bool same_geometry) {
+    const uint32_t n = (uint32_t)m->s.size();
+    const uint32_t W = desc->Width, H = desc->Height, R = desc->BandRows ? desc->BandRows : 8u;
     const uint32_t maxr = max_local_rows(H, R, n);
     const bool want_prev = cam->PreviousImage.Data != nullptr;
-    hipStream_t caller = (hipStream_t)stream;
     const int d0 = m->s[0].ordinal;
     // resident per-device images (a geometry change drops the running means)
     if (!same_geometry) {
@@ -297,8 +369,14 @@ extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_t
         MHIP(hipSetDevice(sh.ordinal));
         if ((size_t)maxr * W * 16u > sh.cap_prev || (size_t)maxr * W * 4u > sh.cap_cur) {
             MHIP(hipStreamSynchronize(sh.stream));
+            MHIP(hipStreamSynchronize(sh.xfer));
             if (const int rc = grow(&sh.prev, &sh.cap_prev, (size_t)maxr * W * 16u)) return rc;
-            if (const int rc = grow(&sh.cur, &sh.cap_cur, (size_t)maxr * W * 4u)) return rc;
+            size_t cap = sh.cap_cur;
+            for (int b = 0; b < kSlots; ++b) {
+                cap = sh.cap_cur;
+                if (const int rc = grow(&sh.cur[b], &cap, (size_t)maxr * W * 4u)) return rc;
+            }
+            sh.cap_cur = cap;
         }
     }
     MHIP(hipSetDevice(d0));
@@ -312,41 +390,52 @@ extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_t
         }
     }
     m->width = W, m->height = H, m->band_rows = R;
-    // every device's work follows the caller's prior work on `stream`, and the
-    // previous call's gather (it read the shard images these traces overwrite)
+    const uint32_t b = m->calls & 1u;
+    // The traces read nothing of the caller's: they wait only until their slot
+    // has been gathered (two calls back) and, when the last call gathered the
+    // resident means they overwrite, until that gather is done.  Everything the
+    // caller sees (frame, mean, d_rays) is written on the gather stream, after
+    // the caller's prior work on `stream`.
     MHIP(hipEventRecord(m->start, caller));
-    uint64_t folded = 0;
+    const uint32_t pb = b ^ 1u;
     for (uint32_t i = 0; i < n; ++i) {
         Shard &sh = m->s[i];
         MHIP(hipSetDevice(sh.ordinal));
-        MHIP(hipStreamWaitEvent(sh.stream, m->start, 0));
-        if (m->gathered_valid) MHIP(hipStreamWaitEvent(sh.stream, m->gathered, 0));
-        MHIP(hipMemsetAsync(sh.rays, 0, sizeof(uint64_t), sh.stream));
+        if (m->slot_used[b]) MHIP(hipStreamWaitEvent(sh.stream, m->transport == RT_MULTI_RCCL ? sh.sent[b] : m->copied[b], 0));
+        if (m->prev_gathered && m->slot_used[pb])
+            MHIP(hipStreamWaitEvent(sh.stream, m->transport == RT_MULTI_RCCL ? sh.sent[pb] : m->copied[pb], 0));
+        MHIP(hipMemsetAsync(sh.rays[b], 0, sizeof(uint64_t), sh.stream));
         rt_camera_info c = *cam;
-        c.CurrentImage.Data = sh.cur;
+        c.CurrentImage.Data = sh.cur[b];
         c.PreviousImage.Data = sh.prev;
         rt_trace_desc d = *desc;
         d.BandRows = R;
         d.BandCount = n;
         d.BandIndex = i;
         if (restart) d.Flags |= RT_FLAG_ACCUM_ZERO;
-        if (const int rc = rt_trace(sh.dev, &c, &d, sh.rays, sh.stream)) return rc;
-        rt_trace_info info;
-        rt_trace_last_info(sh.dev, &info);
-        if (rt_band_local_rows(H, R, n, i) && desc->Frames) folded += info.SegmentsFolded;
-        MHIP(hipEventRecord(sh.traced, sh.stream));
+        MHIP(hipEventRecord(sh.t0[b], sh.stream));
+        if (const int rc = rt_trace(sh.dev, &c, &d, sh.rays[b], sh.stream)) return rc;
+        MHIP(hipEventRecord(sh.t1[b], sh.stream));
+        MHIP(hipEventRecord(sh.traced[b], sh.stream));
+        sh.launched = rt_band_local_rows(H, R, n, i) > 0 && desc->Frames > 0;
     }
     // gather to devices[0]: compact images -> staging (rank-strided), then scatter
     const uint64_t stride_cur = (uint64_t)maxr * W * 4u, stride_prev = (uint64_t)maxr * W * 16u;
     if (m->transport == RT_MULTI_RCCL) {
+        // sends leave from each device's transfer stream, so its next trace
+        // (the other slot) does not queue behind them
+        for (Shard &sh : m->s) {
+            MHIP(hipSetDevice(sh.ordinal));
+            MHIP(hipStreamWaitEvent(sh.xfer, sh.traced[b], 0));
+        }
         const Rccl &r = rccl();
         NCCL_OK(r.GroupStart());
         for (uint32_t i = 0; i < n; ++i) {
             Shard &sh = m->s[i];
             const size_t bc = band_bytes(W, H, R, n, i, 4u);
-            if (bc) NCCL_OK(r.Send(sh.cur, bc, ncclUint8, 0, sh.comm, sh.stream));
-            if (bc && want_prev) NCCL_OK(r.Send(sh.prev, bc * 4u, ncclUint8, 0, sh.comm, sh.stream));
-            NCCL_OK(r.Send(sh.rays, 1, ncclUint64, 0, sh.comm, sh.stream));
+            if (bc) NCCL_OK(r.Send(sh.cur[b], bc, ncclUint8, 0, sh.comm, sh.xfer));
+            if (bc && want_prev) NCCL_OK(r.Send(sh.prev, bc * 4u, ncclUint8, 0, sh.comm, sh.xfer));
+            NCCL_OK(r.Send(sh.rays[b], 1, ncclUint64, 0, sh.comm, sh.xfer));
         }
         for (uint32_t i = 0; i < n; ++i) {
             const size_t bc = band_bytes(W, H, R, n, i, 4u);
@@ -356,19 +445,26 @@ extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_t
             NCCL_OK(r.Recv(m->ray_slots + i, 1, ncclUint64, (int)i, m->s[0].comm, m->gather));
         }
         NCCL_OK(r.GroupEnd());
+        for (Shard &sh : m->s) {
+            MHIP(hipSetDevice(sh.ordinal));
+            MHIP(hipEventRecord(sh.sent[b], sh.xfer));
+        }
         MHIP(hipSetDevice(d0));
     } else {
         MHIP(hipSetDevice(d0));
         for (uint32_t i = 0; i < n; ++i) {
             Shard &sh = m->s[i];
-            MHIP(hipStreamWaitEvent(m->gather, sh.traced, 0));
+            MHIP(hipStreamWaitEvent(m->gather, sh.traced[b], 0));
             const size_t bc = band_bytes(W, H, R, n, i, 4u);
-            if (bc) MHIP(hipMemcpyPeerAsync(m->stage_cur + i * stride_cur, d0, sh.cur, sh.ordinal, bc, m->gather));
+            if (bc) MHIP(hipMemcpyPeerAsync(m->stage_cur + i * stride_cur, d0, sh.cur[b], sh.ordinal, bc, m->gather));
             if (bc && want_prev)
                 MHIP(hipMemcpyPeerAsync(m->stage_prev + i * stride_prev, d0, sh.prev, sh.ordinal, bc * 4u, m->gather));
-            MHIP(hipMemcpyPeerAsync(m->ray_slots + i, d0, sh.rays, sh.ordinal, sizeof(uint64_t), m->gather));
+            MHIP(hipMemcpyPeerAsync(m->ray_slots + i, d0, sh.rays[b], sh.ordinal, sizeof(uint64_t), m->gather));
         }
+        MHIP(hipEventRecord(m->copied[b], m->gather));
     }
+    m->slot_used[b] = true;
+    m->prev_gathered = want_prev;
     MHIP(hipStreamWaitEvent(m->gather, m->start, 0));  // d_rays and the output follow the caller's prior work
     if (rtk_launch_assemble(m->stage_cur, stride_cur, cam->CurrentImage.Data, W, H, 4u, R, n, m->gather) != 0 ||
         (want_prev &&
@@ -376,12 +472,11 @@ extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_t
         rtk_launch_sum_u64(m->ray_slots, n, d_rays, m->gather) != 0)
         return rt_fail(RT_EIO, "rt_multi_trace: gather launch failed: %s", hipGetErrorString(hipGetLastError()));
     MHIP(hipEventRecord(m->gathered, m->gather));
-    m->gathered_valid = true;
     MHIP(hipStreamWaitEvent(caller, m->gathered, 0));
-    m->accum_valid = restart ? desc->Frames > 0 : m->accum_valid;
     m->last_band_rows = R;
     m->last_max_rows = maxr;
-    m->last_folded = folded;
+    m->last_slot = b;
+    m->calls += 1;
     return RT_OK;
 }
 

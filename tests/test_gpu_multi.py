@@ -109,6 +109,60 @@ def test_multi_rejects_continuation_without_a_resident_mean(rt, torch_cuda):
         m.close()
 
 
+def test_multi_rejects_a_wrong_previous_ray_count(rt, torch_cuda):
+    """The resident means hold the frames folded so far; a continuation that
+    claims another count would blend with the wrong weights."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 16)
+    cam = rt.camera_setup(s, 64, 48)
+    m = rt.Multi([0, 0])
+    try:
+        m.upload_scene(s)
+        multi_render(rt, torch, m, cam, 64, 48, 2, 4)
+        with pytest.raises(rt.RtError, match="holds 2 frames"):
+            multi_render(rt, torch, m, cam, 64, 48, 2, 4, prev_count=3)
+        multi_render(rt, torch, m, cam, 64, 48, 3, 4, prev_count=2)
+        multi_render(rt, torch, m, cam, 64, 48, 1, 4, prev_count=5)
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0, 0], [0] * 8])
+def test_multi_calls_back_to_back_overlap_gather_and_trace(rt, orc, torch_cuda, devices):
+    """Calls enqueued back to back with no host synchronisation: each device
+    alternates between two band-image slots, so call k's gather overlaps call
+    k+1's traces and a slot is reused only after the gather two calls back.
+    Five calls with three cameras (new cull keys included) into five frames,
+    each bit-identical to one device's render; per-device trace times exist."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 64)
+    W, H, S, B = 200, 150, 4, 8
+    views = [(None, None), (6.0, 0.7), (None, None), (2.0, -1.1), (None, None)]
+    cams = [rt.camera_setup(s, W, H, distance=d, x_angle=a) for d, a in views]
+    refs = [single(rt, torch, s, c, W, H, S, B) for c in cams[:2]] + [None] + \
+           [single(rt, torch, s, cams[3], W, H, S, B)] + [None]
+    refs[2] = refs[4] = refs[0]
+    m = rt.Multi(devices)
+    try:
+        m.upload_scene(s)
+        outs = []
+        st = torch.cuda.current_stream().cuda_stream
+        for cam in cams:
+            cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            m.trace(cam, width=W, height=H, cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(), frames=S,
+                    max_bounce=B, band_rows=8, accum_zero=True, stream=st)
+            outs.append((cur, rays))
+        ms = m.last_trace_ms(len(devices))
+        torch.cuda.synchronize()
+    finally:
+        m.close()
+    assert len(ms) == len(devices) and all(v >= 0.0 for v in ms)
+    for (cur, rays), ref in zip(outs, refs):
+        assert int(rays.item()) == ref[2]
+        assert torch_equal_bits(cur, ref[1]), "RGBA8 differs"
+
+
 def test_multi_rccl_refuses_a_device_listed_twice(rt, torch_cuda):
     with pytest.raises(rt.RtError, match="RCCL"):
         rt.Multi([0, 0], rt.RT_MULTI_RCCL)

@@ -360,6 +360,74 @@ def test_camera_change_recomputes_the_cull_pass(rt, orc, torch_cuda, gdev):
         assert_same(*g, *r)
 
 
+@pytest.mark.parametrize("simd", [True, False])
+def test_new_cameras_back_to_back_without_host_sync(rt, orc, torch_cuda, monkeypatch, simd):
+    """Three different cameras enqueued back to back with no synchronisation in
+    between: each is a new cull key whose live-tile count stays
+    on the device (grid over every tile, early exit), and its dead-tile segments
+    are added from the device total.  The long launches also take the split
+    head + rest path.  Every frame and count is bit-exact vs the oracle; the
+    folded segments reported afterwards (rt_trace_last_info, which waits for the
+    totals) are the last camera's."""
+    torch = torch_cuda
+    s, o = _scenes(rt, orc, 1, 64)
+    W, H, F, B = 160, 96, 128, 5
+    views = [(None, None), (6.0, 0.7), (2.0, -1.1)]
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", "4")  # P = 4: a 128-frame launch is split (head + rest)
+    dev = rt.Device(0)
+    try:
+        dev.upload_scene(s)
+        stream = torch.cuda.current_stream().cuda_stream
+        outs = []
+        for dist, ang in views:
+            cam = rt.camera_setup(s, W, H, distance=dist, x_angle=ang)
+            prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                      rays_ptr=rays.data_ptr(), frames=F, max_bounce=B, simd=simd, accum_zero=True, stream=stream)
+            outs.append((prev, cur, rays))
+        info = dev.last_info()
+        torch.cuda.synchronize()
+    finally:
+        dev.close()
+    assert info["CullPassRan"] == 1 and info["SplitHeadFrames"] > 0, info
+    for (dist, ang), (prev, cur, rays) in zip(views, outs):
+        r = orc.render(o, orc.camera(o, W, H, distance=dist, x_angle=ang), W, H, frames=F, max_bounce=B, simd=simd)
+        assert_same(prev, cur, int(rays.item()), *r)
+    assert 0 < info["TilesTraced"] <= info["TilesTotal"]
+
+
+def test_stream_switch_keeps_every_bit(rt, orc, torch_cuda):
+    """Launches of one device on two streams in turn: the new stream waits for
+    the old one's last trace on the device (no host synchronisation, the cull
+    masks and learned order are kept)."""
+    torch = torch_cuda
+    s, o = _scenes(rt, orc, 1, 64)
+    W, H = 96, 64
+    cam = rt.camera_setup(s, W, H)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    dev = rt.Device(0)
+    try:
+        dev.upload_scene(s)
+        outs = []
+        for i in range(4):
+            prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                      rays_ptr=rays.data_ptr(), frames=4, max_bounce=5, accum_zero=True,
+                      stream=streams[i % 2].cuda_stream)
+            outs.append((prev, cur, rays))
+        torch.cuda.synchronize()
+    finally:
+        dev.close()
+    r = orc.render(o, orc.camera(o, W, H), W, H, frames=4, max_bounce=5)
+    for prev, cur, rays in outs:
+        assert_same(prev, cur, int(rays.item()), *r)
+
+
 @pytest.mark.parametrize("idx,n,W,H,P", [(1, 64, 96, 64, 4), (1, 128, 16, 16, 1), (1, 200, 40, 32, 2),
                                          (1, 256, 64, 48, 8), (0, None, 48, 32, 16)])
 def test_cull_masks_equal_cpu_restatement(rt, torch_cuda, monkeypatch, idx, n, W, H, P):
