@@ -214,9 +214,14 @@ def valu_roofline(pmc, kern_ms: float):
            "wave_cycles_issue_stalled": round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4),
            "salu_per_valu": round(c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"], 4),
            "gpu_cycles_per_launch": cycles}
-    if "SQ_ACTIVE_INST_SCA" in c and "SQ_BUSY_CYCLES" in c:
-        # scalar unit: one per CU (256), SQ_ACTIVE_INST_SCA in quad-cycles like the VALU counter
-        out["salu_issue_occupancy"] = round(c["SQ_ACTIVE_INST_SCA"] / (256 * cycles / 4.0), 4)
+    # the scalar unit: one per CU (256), at most one SALU instruction per CU cycle (the
+    # sequencer serves the CU's four SIMDs in turn, one scalar issue each); SQ_ACTIVE_INST_SCA
+    # counts wave quad-cycles like the VALU counter (so per SIMD)
+    out["salu_per_cu_cycle"] = round(c["SQ_INSTS_SALU"] / (256.0 * cycles), 4)
+    if "SQ_ACTIVE_INST_SCA" in c:
+        out["sca_active_per_simd_quad_cycle"] = round(c["SQ_ACTIVE_INST_SCA"] / (SIMDS * cycles / 4.0), 4)
+    if "SQ_INSTS_SMEM" in c:
+        out["smem_per_cu_cycle"] = round(c["SQ_INSTS_SMEM"] / (256.0 * cycles), 4)
     return out
 
 

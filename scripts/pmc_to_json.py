@@ -2,7 +2,8 @@
 record for the trace kernel that bench.py reports as roofline.traffic and as
 the executed-work roofline fraction.
 
-usage: python scripts/pmc_to_json.py gpurun_out pmc_r02_c2_ profiles/r02_c2_pmc.json "<workload>"
+usage: python scripts/pmc_to_json.py gpurun_out pmc_r02_c2_ profiles/r02_c2_pmc.json "<workload>" [bands]
+(bands: the band split of a --sim-ranks share, e.g. 8; bench.py matches records on workload + bands)
 
 Per pass only the LAST trace_kernel dispatch is kept (the bench's timed, warm
 launch; the earlier ones are the cold launch and warm-up launches that learn
@@ -24,6 +25,7 @@ import json
 import sys
 
 root, prefix, out, workload = sys.argv[1:5]
+bands = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 per = {}
 kernel = None
 for f in sorted(glob.glob(f"{root}/{prefix}*/**/*counter_collection.csv", recursive=True)):
@@ -44,7 +46,7 @@ for f in sorted(glob.glob(f"{root}/{prefix}*/**/*counter_collection.csv", recurs
 g = per.pop("GRBM_GUI_ACTIVE_passes", [])
 if g:
     per["GRBM_GUI_ACTIVE"] = sum(g) / len(g)
-rec = {"workload": workload, "kernel": kernel, "dispatch": "last trace_kernel dispatch of each pass (warm)",
+rec = {"workload": workload, "bands": bands, "kernel": kernel, "dispatch": "last trace_kernel dispatch of each pass (warm)",
        "counters_per_dispatch": per}
 if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     rec["hbm_bytes_per_dispatch"] = 2.0 * per["FETCH_SIZE"] * 1024 + per["WRITE_SIZE"] * 1024

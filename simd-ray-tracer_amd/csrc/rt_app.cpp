@@ -71,18 +71,23 @@ struct App {
     float distance = 0.0f, x_angle = 0.0f, y_height = 0.0f;
     uint32_t prev_count = 0;
     uint32_t width = 0, height = 0;
-    void *d_prev = nullptr, *d_cur = nullptr;
+    // Two device frames: frame k writes d_cur[k & 1] while the completed frame
+    // k - 1 is handed out from the other, so a call launches the next frame
+    // FIRST and then copies the previous one to the caller's image (the
+    // reference's CopyImage, main.cpp:688-697) while the GPU traces.
+    void *d_prev = nullptr;
+    uint32_t *d_cur[2] = {nullptr, nullptr};
+    uint32_t slot = 0;             // d_cur slot of the last launched frame
     uint64_t *d_rays = nullptr;
-    // Each launched frame is followed on the stream by asynchronous copies of
-    // its RGBA8 image and ray count into pinned host memory, so a completed
-    // frame is already on the host: handing it out is the reference's
-    // CopyImage (main.cpp:688-697), a host copy, with no GPU round trip.
-    uint32_t *h_frame = nullptr;  // pinned, width x height
-    uint64_t *h_rays = nullptr;   // pinned
-    bool h_valid = false;         // h_frame / h_rays hold the last launched frame (once complete)
+    uint64_t *h_rays = nullptr;    // pinned: the last frame's count, copied after its trace
     hipEvent_t ev_start = nullptr, ev_done = nullptr;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // traces
+    hipStream_t copy = nullptr;    // the hand-out DMA, beside the next frame's trace
     bool in_flight = false;
+    // The caller's image is page-locked (hipHostRegister) once the same buffer
+    // comes back a second time, so the hand-out is one DMA straight into it.
+    void *seen_ptr = nullptr, *reg_ptr = nullptr;
+    size_t seen_bytes = 0, reg_bytes = 0;
     rt_camera_info cam;
     rt_on_render_profile prof;
 };
@@ -109,16 +114,35 @@ int wait_frame() {
     return RT_OK;
 }
 
-// The completed frame into the caller's image: CopyImage of main.cpp:688-697
-// from the pinned copy the frame's own stream work already made.
-int copy_current(const rt_image *image) {
+void unregister_image() {
+    if (g_app.reg_ptr) (void)hipHostUnregister(g_app.reg_ptr);
+    (void)hipGetLastError();
+    g_app.reg_ptr = nullptr;
+    g_app.reg_bytes = 0;
+}
+
+// The completed frame in d_cur[slot] into the caller's image (CopyImage,
+// main.cpp:688-697): one DMA on the copy stream, into the page-locked image
+// when the caller keeps passing the same buffer (else HIP stages it).
+int hand_out(const rt_image *image, uint32_t slot) {
     if (!image->Data) return RT_OK;
     const size_t bytes = (size_t)g_app.width * g_app.height * 4u;
     const double t = now_ms();
-    if (g_app.h_valid)
-        memcpy(image->Data, g_app.h_frame, bytes);
-    else
-        memset(image->Data, 0, bytes);  // nothing traced yet: the zero-filled CurrentImage
+    if (image->Data == g_app.seen_ptr && bytes == g_app.seen_bytes &&
+        (image->Data != g_app.reg_ptr || bytes != g_app.reg_bytes)) {
+        unregister_image();
+        if (hipHostRegister(image->Data, bytes, hipHostRegisterDefault) == hipSuccess) {
+            g_app.reg_ptr = image->Data;
+            g_app.reg_bytes = bytes;
+        } else {
+            (void)hipGetLastError();  // stays pageable: the staged copy below still works
+        }
+    }
+    g_app.seen_ptr = image->Data;
+    g_app.seen_bytes = bytes;
+    if (hipMemcpyAsync(image->Data, g_app.d_cur[slot], bytes, hipMemcpyDeviceToHost, g_app.copy) != hipSuccess ||
+        hipStreamSynchronize(g_app.copy) != hipSuccess)
+        return RT_EIO;
     g_app.prof.HostCopyMs += now_ms() - t;
     g_app.prof.FramesCopied += 1;
     return RT_OK;
@@ -161,7 +185,8 @@ extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices
     if (hipMalloc(&g_app.d_rays, sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc(&g_app.h_rays, sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&g_app.ev_start) != hipSuccess || hipEventCreate(&g_app.ev_done) != hipSuccess ||
-        hipStreamCreateWithFlags(&g_app.stream, hipStreamNonBlocking) != hipSuccess)
+        hipStreamCreateWithFlags(&g_app.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&g_app.copy, hipStreamNonBlocking) != hipSuccess)
         return RT_ENOMEM;
     (void)hipMemset(g_app.d_rays, 0, sizeof(uint64_t));
     g_app.ready = true;
@@ -214,42 +239,38 @@ static int on_render(const rt_image *image, rt_render_params params, uint32_t ke
     const bool complete = frame_complete();                                          // :783
     const bool resize = image->Width != g_app.width || image->Height != g_app.height;  // :784
     bool copy_out = complete && !resize;
-    if (copy_out && copy_current(image) != RT_OK) return RT_EIO;
     if (resize || moved || (keys & RT_KEY_RESET)) {  // :791-804
         if (wait_frame() != RT_OK) return RT_EIO;
-        if (!resize) {
-            if (copy_current(image) != RT_OK) return RT_EIO;
-            copy_out = true;
-        }
+        copy_out = !resize;  // the completed frame still goes out (below)
         g_app.prev_count = 0;
-        const size_t px = (size_t)image->Width * image->Height;
         if (resize) {
+            const size_t px = (size_t)image->Width * image->Height;
             (void)hipFree(g_app.d_prev);
-            (void)hipFree(g_app.d_cur);
-            if (g_app.h_frame) (void)hipHostFree(g_app.h_frame);
-            g_app.d_prev = g_app.d_cur = nullptr;
-            g_app.h_frame = nullptr;
-            g_app.h_valid = false;
-            if (hipMalloc(&g_app.d_prev, px * 16u) != hipSuccess || hipMalloc(&g_app.d_cur, px * 4u) != hipSuccess ||
-                hipHostMalloc(&g_app.h_frame, px * 4u, hipHostMallocDefault) != hipSuccess)
+            (void)hipFree(g_app.d_cur[0]);
+            (void)hipFree(g_app.d_cur[1]);
+            g_app.d_prev = g_app.d_cur[0] = g_app.d_cur[1] = nullptr;
+            if (hipMalloc(&g_app.d_prev, px * 16u) != hipSuccess || hipMalloc(&g_app.d_cur[0], px * 4u) != hipSuccess ||
+                hipMalloc(&g_app.d_cur[1], px * 4u) != hipSuccess)
                 return RT_ENOMEM;
             g_app.width = image->Width;
             g_app.height = image->Height;
+            g_app.in_flight = false;
         }
-        // the arena zero-fills on Push (wasm/wasm.cpp:52)
-        if (hipMemsetAsync(g_app.d_prev, 0, px * 16u, g_app.stream) != hipSuccess ||
-            hipMemsetAsync(g_app.d_cur, 0, px * 4u, g_app.stream) != hipSuccess)
-            return RT_EIO;
+        // (the reference's arena zero-fills the new images on Push, wasm/wasm.cpp:52;
+        // here the restarted frame writes every pixel of both, and PreviousRayCount 0
+        // keeps the old running mean from being read, so no clear is needed)
     } else if (complete) {
         g_app.prev_count += 1;  // :805-806
     } else {
         return 0;  // :807-808
     }
+    const uint32_t done_slot = g_app.slot;  // the completed frame (when copy_out)
+    const uint32_t slot = g_app.in_flight ? done_slot ^ 1u : done_slot;
     rt_scene sc;
     rt_scene_builtin(g_app.scene_index, &sc);
     int rc = rt_camera_setup(&sc, g_app.distance, g_app.x_angle, g_app.y_height, g_app.width, g_app.height, &g_app.cam);
     if (rc) return rc;
-    g_app.cam.CurrentImage.Data = g_app.d_cur;
+    g_app.cam.CurrentImage.Data = g_app.d_cur[slot];
     g_app.cam.CurrentImage.Width = g_app.width;
     g_app.cam.CurrentImage.Height = g_app.height;
     g_app.cam.CurrentImage.Format = RT_FORMAT_R8G8B8A8_U32;
@@ -257,7 +278,7 @@ static int on_render(const rt_image *image, rt_render_params params, uint32_t ke
     g_app.cam.PreviousImage.Width = g_app.width;
     g_app.cam.PreviousImage.Height = g_app.height;
     g_app.cam.PreviousImage.Format = RT_FORMAT_R32B32G32A32_F32;
-    if (copy_out && out_total_rays_cast) *out_total_rays_cast = g_app.h_valid ? *g_app.h_rays : 0u;  // :840-842
+    if (copy_out && out_total_rays_cast) *out_total_rays_cast = g_app.in_flight ? *g_app.h_rays : 0u;  // :840-842
     {  // :848 (the previous frame has completed here: on every path above)
         float ms = 0.0f;
         if (g_app.in_flight && hipEventElapsedTime(&ms, g_app.ev_start, g_app.ev_done) != hipSuccess) {
@@ -267,6 +288,7 @@ static int on_render(const rt_image *image, rt_render_params params, uint32_t ke
         g_app.prof.GpuFrameMs += ms;
         if (out_time_elapsed_ms) *out_time_elapsed_ms = ms;
     }
+    const bool had_frame = g_app.in_flight;
     if (hipMemsetAsync(g_app.d_rays, 0, sizeof(uint64_t), g_app.stream) != hipSuccess) return RT_EIO;  // :843-846
     rt_trace_desc desc;
     memset(&desc, 0, sizeof(desc));
@@ -289,15 +311,20 @@ static int on_render(const rt_image *image, rt_render_params params, uint32_t ke
         rc = rt_trace(g_app.dev, &g_app.cam, &desc, g_app.d_rays, g_app.stream);
     }
     if (rc) return rc;
-    // the frame's image and count follow it to the host (the next call hands them out)
-    if (hipMemcpyAsync(g_app.h_frame, g_app.d_cur, (size_t)g_app.width * g_app.height * 4u, hipMemcpyDeviceToHost,
-                       g_app.stream) != hipSuccess ||
-        hipMemcpyAsync(g_app.h_rays, g_app.d_rays, sizeof(uint64_t), hipMemcpyDeviceToHost, g_app.stream) != hipSuccess)
+    if (hipMemcpyAsync(g_app.h_rays, g_app.d_rays, sizeof(uint64_t), hipMemcpyDeviceToHost, g_app.stream) != hipSuccess ||
+        hipEventRecord(g_app.ev_done, g_app.stream) != hipSuccess)
         return RT_EIO;
-    if (hipEventRecord(g_app.ev_done, g_app.stream) != hipSuccess) return RT_EIO;
-    g_app.h_valid = true;
+    g_app.slot = slot;
     g_app.in_flight = true;
     g_app.prof.FramesLaunched += 1;
+    // the completed frame goes out while the new one traces (it is in the other slot)
+    if (copy_out) {
+        if (!had_frame) {  // nothing traced yet: the zero-filled CurrentImage
+            if (image->Data) memset(image->Data, 0, (size_t)g_app.width * g_app.height * 4u);
+        } else if (hand_out(image, done_slot) != RT_OK) {
+            return RT_EIO;
+        }
+    }
     return copy_out ? 1 : 0;
 }
 
@@ -313,14 +340,16 @@ extern "C" int rt_on_render_wait(void) { return g_app.ready ? wait_frame() : RT_
 extern "C" int rt_on_shutdown(void) {
     if (!g_app.ready) return RT_OK;
     wait_frame();
+    unregister_image();
     (void)hipFree(g_app.d_prev);
-    (void)hipFree(g_app.d_cur);
+    (void)hipFree(g_app.d_cur[0]);
+    (void)hipFree(g_app.d_cur[1]);
     (void)hipFree(g_app.d_rays);
-    if (g_app.h_frame) (void)hipHostFree(g_app.h_frame);
     if (g_app.h_rays) (void)hipHostFree(g_app.h_rays);
     (void)hipEventDestroy(g_app.ev_start);
     (void)hipEventDestroy(g_app.ev_done);
     (void)hipStreamDestroy(g_app.stream);
+    if (g_app.copy) (void)hipStreamDestroy(g_app.copy);
     rt_device_destroy(g_app.dev);
     rt_multi_destroy(g_app.multi);
     g_app = App();

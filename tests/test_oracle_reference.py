@@ -212,3 +212,92 @@ def test_horizontal_min_vs_reference(orc, refmath):
         m = orc.lib().or_horizontal_min(v.ctypes.data, ctypes.byref(lane))
         assert bits(m) == bits(refmath.ref_horizontal_min(v.ctypes.data))
         assert lane.value == int(np.flatnonzero(v == np.float32(m))[0])
+
+
+# ---- the scenes' RNG-drawn colours, restated from main.cpp's text and drawn with the
+# reference's own compiled RandomFloat (librefmath): pins the palette that no ray count sees
+def _ref_rng(refmath, seed):
+    state = ctypes.c_uint64(seed)
+
+    def draw(lo=-1.0, hi=1.0):  # u32_random_state::RandomFloat(Min, Max), base.h:983-989
+        return np.float32(refmath.ref_random_float(ctypes.byref(state), lo, hi))
+    return draw
+
+
+def test_floating_spheres_palette_from_reference_rng(rt, orc, refmath):
+    """main.cpp:109-131 (Materials[28]: Color in (0.15,1) x (0.1,0.75) x (0.15,1),
+    emission RandomFloat(2, 5) * Color with probability 1/8, else Specular 1 with
+    probability 0.65) and main.cpp:133-152 (sphere i < 3 takes Materials[0], sphere
+    i >= 3 Materials[i % 28]): every sphere's Color, Emissive and Specular in the
+    library's and the oracle's scene 1 equal these draws bit for bit."""
+    draw = _ref_rng(refmath, 0x29D7A0A514F22432)
+    pal = []
+    for _ in range(28):
+        c = np.array([draw(0.15, 1.0), draw(0.1, 0.75), draw(0.15, 1.0)], np.float32)
+        e = np.zeros(3, np.float32)
+        spec = np.float32(0.0)
+        if draw(0.0) < np.float32(0.125):
+            e = (draw(2.0, 5.0) * c).astype(np.float32)
+        elif draw(0.0) < np.float32(0.65):
+            spec = np.float32(1.0)
+        pal.append((c, e, spec))
+    assert sum(1 for p in pal if p[1].any()) > 0 and sum(1 for p in pal if p[2] == 1.0) > 0
+    sp, _, ma = rt.scene_arrays(rt.scene_builtin(1))
+    o = orc.scene_builtin(1)
+    for i in range(256):
+        c, e, spec = pal[0 if i < 3 else i % 28]
+        for arr, name in ((sp, "library"), (o.spheres, "oracle")):
+            row = arr[i]
+            assert np.array_equal(row[8:11].view(np.uint32), c.view(np.uint32)), (name, i, "Color")
+            assert np.array_equal(row[12:15].view(np.uint32), e.view(np.uint32)), (name, i, "Emissive")
+            assert row[16] == spec and row[17] == 0.0, (name, i, "Specular/IOR")
+        for arr, name in ((ma, "library"), (o.materials, "oracle")):
+            assert np.array_equal(arr[i, 0:3].view(np.uint32), c.view(np.uint32)), (name, i, "material Color")
+            assert np.array_equal(arr[i, 4:7].view(np.uint32), e.view(np.uint32)), (name, i, "material Emissive")
+
+
+def test_rtweekend_draws_from_reference_rng(rt, orc, refmath):
+    """main.cpp:221-262: for each (i, j) in [-11, 11)^2, M = RandomFloat(0, 1);
+    centres redrawn (i + RandomFloat(), 0.2, j + RandomFloat()) while within 0.9
+    (v3::Length, compared in double) of (4, 0.2, 0), (0, 0.2, 0) or (-4, 0.2, 0);
+    then M < 0.8: Color = 3 x RandomFloat(0, 1); M < 0.95: the same plus Specular =
+    RandomFloat(0.5, 1); else glass (Color 1, IOR 1.5).  Positions x WorldScale
+    (CreateScalarSphere, main.cpp:56-70).  The 478 spheres the scene keeps (after
+    the 4 fixed ones) must equal these draws in the library and the oracle."""
+    draw = _ref_rng(refmath, 0xCD46749A57ACB371)
+    F = np.float32
+    ws = F(1.0 / 16.0)
+
+    def length(v):  # v3::Length = SquareRoot(Dot(v, v)), x64_math.h:228-232
+        a = (ctypes.c_float * 3)(*[float(x) for x in v])
+        return refmath.ref_sqrt(refmath.ref_dot(a, a))
+
+    want = []
+    for i in range(-11, 11):
+        for j in range(-11, 11):
+            m = draw(0.0, 1.0)
+            while True:
+                c = np.array([F(i) + draw(), F(0.2), F(j) + draw()], F)
+                ok = all(float(length((c - np.array(q, F)).astype(F))) > 0.9
+                         for q in ((4, 0.2, 0), (0, 0.2, 0), (-4, 0.2, 0)))
+                if ok:
+                    break
+            spec, ior = F(0.0), F(0.0)
+            if float(m) < 0.8:
+                col = np.array([draw(0.0, 1.0), draw(0.0, 1.0), draw(0.0, 1.0)], F)
+            elif float(m) < 0.95:
+                col = np.array([draw(0.0, 1.0), draw(0.0, 1.0), draw(0.0, 1.0)], F)
+                spec = draw(0.5, 1.0)
+            else:
+                col, ior = np.ones(3, F), F(1.5)
+            want.append(((c * ws).astype(F), col, spec, ior))
+    sp, _, _ = rt.scene_arrays(rt.scene_builtin(2))
+    o = orc.scene_builtin(2).spheres
+    assert len(sp) == 482
+    for k in range(478):
+        pos, col, spec, ior = want[k]
+        for arr, name in ((sp, "library"), (o, "oracle")):
+            row = arr[4 + k]
+            assert np.array_equal(row[0:3].view(np.uint32), pos.view(np.uint32)), (name, k, "Position")
+            assert np.array_equal(row[8:11].view(np.uint32), col.view(np.uint32)), (name, k, "Color")
+            assert row[16].view(np.uint32) == spec.view(np.uint32) and row[17] == ior, (name, k, "Specular/IOR")
