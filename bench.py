@@ -603,7 +603,14 @@ def main():
             gbuf = [torch.empty((world, maxr * W), dtype=torch.int32, device=gdev) for _ in range(2)]
     side = torch.cuda.Stream() if comm else None
     gathered = [None, None]  # per slot: event after its gather on the side stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events around every timed launch give the kernel's own average time on
+    # one whole-frame GPU (the roofline's denominator).  A band share (world > 1 or
+    # --sim-ranks) takes one pair around the whole timed loop instead: every event
+    # marker between launches widens the dispatch gap (measured ~4.6 us each), a
+    # measurable share of a 0.8 ms launch; its kernel time is then GPU ms per step.
+    per_launch_events = world == 1 and bands == 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps if per_launch_events else 1)]
     state = {"n": 0, "pending": None, "c": 0}
 
     def finish():  # frame whose gather is in flight -> assembled on rank 0
@@ -624,14 +631,14 @@ def main():
             stream.wait_event(gathered[slot])
         c = state["c"]
         state["c"] += 1
-        if i is not None:
+        if i is not None and (per_launch_events or i == 0):
             ev[i][0].record(stream)
         dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur[slot].data_ptr(),
                   rays_ptr=ctr[c].data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
                   band_rows=band_rows, band_count=bands, band_index=band_index, accum_zero=True,
                   stream=stream.cuda_stream)
-        if i is not None:
-            ev[i][1].record(stream)
+        if i is not None and (per_launch_events or i == args.steps - 1):
+            ev[i if per_launch_events else 0][1].record(stream)
         if world > 1 and comm is not None:
             traced = torch.cuda.Event()
             traced.record(stream)

@@ -210,9 +210,10 @@ uint32_t rt_band_local_rows(uint32_t height, uint32_t band_rows, uint32_t band_c
  * this device runs the primary-ray cull pass; its live-tile count stays on
  * the device (the trace grid covers every tile and blocks past the count
  * exit) until it has reached the host asynchronously, after which launches
- * of the same key size their grids exactly.  When the stream changes between
- * launches, the new stream waits (device-side) for the old one's last trace.
- * (Buffer growth for a larger geometry than any before is the one host wait.) */
+ * of the same key size their grids exactly.  Launches of one device are meant
+ * for one stream: when the stream changes between launches, the call first
+ * waits for the device (host-side), as it does when it grows its buffers for
+ * a larger geometry than any before.  PreviousRayCount + Frames must fit a u32. */
 int rt_trace(rt_device *dev, const rt_camera_info *cam, const rt_trace_desc *desc,
              uint64_t *d_rays, void *stream);
 

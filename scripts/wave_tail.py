@@ -1,6 +1,8 @@
 """Diagnostic: per-wave start/end times of one C2 launch -> occupancy over time.
 env: SPP (256), SIM_RANKS (1: whole frame; G: rank 0's bands of a G-GPU split),
-RT_LANES_PER_PIXEL (auto), LAUNCHES (8: the learned order settles)."""
+RT_LANES_PER_PIXEL (auto), LAUNCHES (8: the learned order settles), SAVE (a .npz
+path: the raw per-wave {start, end} of the last launch, indexed 4 * block tile + wave,
+for offline schedule simulation: scripts/sched_sim.py)."""
 import os
 import sys
 import pathlib
@@ -25,6 +27,8 @@ for _ in range(int(os.environ.get("LAUNCHES", "8"))):
               frames=S, max_bounce=B, accum_zero=True, band_rows=8, band_count=G, band_index=0)
 torch.cuda.synchronize()
 wt_all = dev.debug_wave_times().astype(np.int64)
+if os.environ.get("SAVE"):
+    np.savez_compressed(os.environ["SAVE"], wave_times=wt_all, info=np.array(list(dev.last_info().values())))
 wt = wt_all[wt_all[:, 1] > 0]
 t0 = wt[:, 0].min()
 st, en = (wt[:, 0] - t0) / 100.0, (wt[:, 1] - t0) / 100.0  # microseconds

@@ -97,6 +97,17 @@ __device__ __forceinline__ float div_rn(float a, float b, float y) {
     return __builtin_fmaf(__builtin_fmaf(-q0, b, a), y, q0);
 }
 
+// The running-mean weights of the frame after pc folded ones (main.cpp:484-487):
+// {RN(1 / (f32)(pc + 1)), RN((f32)pc / (f32)(pc + 1))}, the reference's f32
+// divisions, by the short sequences: n = (f32)(pc + 1) is in [1, 2^32], inside
+// rcp_rn's verified range, so RN(1/n) is rcp_rn(n) itself, and pc / n is +0 or
+// >= 1/2 (div_rn's condition).  (The host keeps pc + 1 below 2^32: rt_trace.)
+__device__ __forceinline__ float2 fold_weights(uint32_t pc) {
+    const float n = (float)(pc + 1u);
+    const float y = rcp_rn(n);
+    return make_float2(y, div_rn((float)pc, n, y));
+}
+
 // v3::Normalize (x64_math.h:234-245): IEEE divide by the correctly rounded
 // sqrt, zero when len^2 <= 1e-4.  Fast path: one reciprocal shared by the
 // three quotients; lanes outside its proven range (a quotient below 2^-99
@@ -1028,8 +1039,7 @@ void trace_kernel(TraceArgs a) {
                 if (q < fold_n) {
                     ratio = fold[q].y;
                 } else {
-                    const uint32_t pc = a.prev_count + q;
-                    ratio = (float)pc / (float)(pc + 1u);
+                    ratio = fold_weights(a.prev_count + q).y;
                 }
                 accx = 0.0f + accx * ratio;
                 accy = 0.0f + accy * ratio;
@@ -1259,9 +1269,8 @@ void trace_kernel(TraceArgs a) {
                     const float oz = a.max_bounce == 0 ? 0.0f : p.cz;
                     if (P == 1) {
                         // ---- running-mean blend (main.cpp:484-489), in order by construction
-                        const uint32_t pc = a.prev_count + k;
-                        const float inv = k < fold_n ? fold[k].x : 1.0f / (float)(pc + 1u);
-                        const float ratio = k < fold_n ? fold[k].y : (float)pc / (float)(pc + 1u);
+                        const float2 fw = k < fold_n ? fold[k] : fold_weights(a.prev_count + k);
+                        const float inv = fw.x, ratio = fw.y;
                         accx = ox * inv + accx * ratio;
                         accy = oy * inv + accy * ratio;
                         accz = oz * inv + accz * ratio;
@@ -1269,10 +1278,8 @@ void trace_kernel(TraceArgs a) {
                     } else {
                         // park Out*(1/n) and the ratio (n-1)/n of sample k's blend; the
                         // sign bit of .w marks the slot ready (the ratio is >= 0)
-                        const uint32_t pc = a.prev_count + k;
                         float2 w = fold[k < fold_n ? k : 0u];  // (fold_n = 0: an unused in-bounds read)
-                        if (__builtin_expect(k >= fold_n, 0))
-                            w = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
+                        if (__builtin_expect(k >= fold_n, 0)) w = fold_weights(a.prev_count + k);
                         ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
                     k += P;

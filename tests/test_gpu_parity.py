@@ -348,6 +348,29 @@ def test_dead_tiles_fold_a_nonzero_running_mean(rt, orc, torch_cuda, gdev):
     assert_same(*g, *r)
 
 
+@pytest.mark.parametrize("prev_count,P", [(1000003, 4), (16777217, 16), (300000001, 1), (4294967000, 8)])
+def test_running_mean_weights_at_large_previous_counts(rt, orc, torch_cuda, monkeypatch, prev_count, P):
+    """The fold weights RN(1/(f32)(n)) and RN((f32)(n-1)/(f32)(n)) (main.cpp:484-487)
+    come from rcp_rn / div_rn (rt_kernel.hip fold_weights) in the one-wave kernels:
+    frames far past the 256-entry weight table, including counts whose f32 conversion
+    rounds (> 2^24) and the top of the u32 range, against the oracle's IEEE divisions,
+    with a random non-zero running mean, every lane shape's blend path."""
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", str(P))
+    s, o = _scenes(rt, orc, 1, 64)
+    W, H = 64, 48
+    cam = rt.camera_setup(s, W, H)
+    rng = np.random.default_rng(prev_count % 1000)
+    prev_np = rng.uniform(0.0, 2.0, (W * H, 4)).astype(np.float32)
+    prev = torch_cuda.from_numpy(prev_np.copy()).to("cuda")
+    dev = rt.Device(0)
+    try:
+        g = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=P, bounces=4, prev_count=prev_count, prev=prev)
+    finally:
+        dev.close()
+    r = orc.render(o, orc.camera(o, W, H), W, H, prev_count=prev_count, frames=P, max_bounce=4, prev=prev_np.copy())
+    assert_same(*g, *r)
+
+
 def test_camera_change_recomputes_the_cull_pass(rt, orc, torch_cuda, gdev):
     """The cull masks and live-tile list are cached per camera / scene /
     geometry: moving the camera between launches on one device must re-cull."""
