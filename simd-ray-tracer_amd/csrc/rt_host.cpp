@@ -48,6 +48,7 @@ struct rt_device {
     int scene_global_env = 0;  // RT_SCENE_GLOBAL=1: keep the scene in HBM even when the LDS image could hold it
     int tables_global_env = 0;  // RT_TABLES_LDS=0: the rsqrt and fold-weight tables stay out of the LDS image
     int solo_env = 1;           // RT_SOLO=0: four waves per workgroup sharing an LDS image (TraceArgs.solo)
+    int wave_order_env = 1;     // RT_WAVE_ORDER=0: one-wave kernels order block tiles, not waves (A/B)
     int walk_any_env = 0;       // RT_WALK_ANY=1: the one-wave kernel dispatches the walk at run time (A/B)
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
     // heaviest-first tile order learned from the previous launch of the same
@@ -175,6 +176,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (sg && sg[0] == '1') d->scene_global_env = 1;
     const char *tl = getenv("RT_TABLES_LDS");  // 0: rsqrt + fold tables read through the caches at every size (A/B)
     if (tl && tl[0] == '0') d->tables_global_env = 1;
+    const char *wo = getenv("RT_WAVE_ORDER");
+    if (wo && wo[0] == '0') d->wave_order_env = 0;
     const char *wa = getenv("RT_WALK_ANY");
     if (wa && wa[0] == '1') d->walk_any_env = 1;
     const char *so = getenv("RT_SOLO");
@@ -879,6 +882,10 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     }
     const int src = a.scene_in_lds ? d->src : kSrcSmem;  // a scene in HBM is read through the scalar cache
     const uint32_t n_tiles = rtk_tile_count(desc->Width, local_rows, lpp);
+    // Units of the heaviest-first order: waves for the one-wave kernels (each wave
+    // its own workgroup, so each is placed by its own cost), block tiles otherwise
+    a.unit_waves = a.solo && d->wave_order_env ? 1u : 0u;
+    const uint32_t n_units = a.unit_waves ? 4u * n_tiles : n_tiles;
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     const bool cull = d->cull != 0;
     const bool empty_capable = cull && !d->use_sky && desc->MaxBounce != 0;
@@ -886,7 +893,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.tiles_x = rtk_tiles_x(desc->Width, lpp);
     std::vector<uint32_t> key = {desc->Width, desc->Height, local_rows, band_rows, band_count, desc->BandIndex,
                                  (uint32_t)lpp, (uint32_t)rs, (uint32_t)cull, (uint32_t)empty_capable, (uint32_t)sched,
-                                 a.interleave,
+                                 a.interleave, a.unit_waves,
                                  (uint32_t)d->scene_gen, (uint32_t)(d->scene_gen >> 32)};
     for (const float *f : {a.cam_pos, a.cam_x, a.cam_y, a.film_center}) {
         for (int i = 0; i < 3; ++i) {
@@ -915,10 +922,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             (void)hipFree(*b);
             *b = nullptr;
         }
-        if (hipMalloc(&d->d_tile_cost, n_tiles * 4u) != hipSuccess ||
-            hipMalloc(&d->d_tile_order, n_tiles * 4u) != hipSuccess ||
+        // cost / order / sort scratch per unit: up to 4 per block tile (wave units)
+        if (hipMalloc(&d->d_tile_cost, 4u * n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_order, 4u * n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
-            hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(n_tiles)) != hipSuccess)
+            hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(4u * n_tiles)) != hipSuccess)
             return fail(RT_ENOMEM, "rt_trace: tile order buffers");
         if (!d->d_cull_counters && hipMalloc(&d->d_cull_counters, kCullCounterWords * 8u) != hipSuccess)
             return fail(RT_ENOMEM, "rt_trace: tile order buffers");
@@ -945,7 +953,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             d->mask_words = mask_words;
             if (rtk_launch_cull(&a, lpp, d->d_tile_live, d->d_tile_cost, d->d_cull_counters, empty_capable ? 1 : 0, s) !=
                     0 ||
-                rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
+                rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_units, s) != 0)
                 return fail(RT_EIO, "rt_trace: cull pass launch failed: %s", hipGetErrorString(hipGetLastError()));
             // the totals follow asynchronously (resolve_counts); no host wait here
             HIP_OK(hipMemcpyAsync(d->h_counts, d->d_cull_counters + kCullTotals, 2 * sizeof(unsigned long long),
@@ -974,7 +982,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
                 head_frames = used;
             }
         } else {
-            HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_tiles * 4u, s));
+            HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_units * 4u, s));
             d->n_live = n_tiles;
             d->dead_pixels = 0;
             d->counts_known = true;
@@ -1024,7 +1032,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         // of an 8-rank C2 share) are skipped
         if (sched && any_live && (d->n_sorts < d->order_launches || part + 1 < n_split)) {
             d->n_sorts += 1;
-            if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_tiles, s) != 0)
+            if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_units, s) != 0)
                 return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
             d->tile_order_valid = true;
         }

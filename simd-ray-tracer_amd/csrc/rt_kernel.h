@@ -75,6 +75,9 @@ struct TraceArgs {
     // optional: live block tiles of the cull pass, on the device (kCullTotals).  Set while the host
     // has not read the count back: the grid then covers every tile and blocks past the count exit.
     const unsigned long long *live_total;
+    // one-wave kernels (solo): tile_order / tile_cost index WAVES (4 * block tile + quadrant),
+    // so the heaviest-first order ranks every wave on its own cost (rt_host.cpp unit_waves)
+    uint32_t unit_waves;
 };
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)
 // striped image pixels of dead block tiles, then the two totals at kCullTotals

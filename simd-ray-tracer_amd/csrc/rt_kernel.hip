@@ -861,6 +861,12 @@ constexpr uint32_t kFoldTable = 256;
 #ifndef RTK_RING_SMALL_P  // ring slots per pixel for P <= 4 (A/B)
 #define RTK_RING_SMALL_P 16
 #endif
+#ifndef RTK_FOLD3  // 1: three lanes of a pixel fold one colour channel each (P >= 4; A/B)
+#define RTK_FOLD3 1
+#endif
+#ifndef RTK_FOLD_FRONTIER  // 1: ring readiness from the lanes' sample cursors, not per-slot flags (A/B)
+#define RTK_FOLD_FRONTIER 1
+#endif
 #ifndef RTK_FOLD_BATCH_SMALL_P  // ring slots the owner reads per LDS round trip at P <= 4 (A/B)
 #define RTK_FOLD_BATCH_SMALL_P 2
 #endif
@@ -959,20 +965,30 @@ void trace_kernel(TraceArgs a) {
             const uint32_t pc = a.prev_count + i;
             fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
         }
-        if (P > 1)
+        if (P > 1 && !RTK_FOLD_FRONTIER)  // (the flag protocol needs clear flags; the frontier reads only parked slots)
             for (uint32_t i = threadIdx.x; i < kWB * kRing * kRingStride; i += blockDim.x)
                 s_ring[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 
     // wave: quadrant of the block tile; sw: the wave's LDS slot in its workgroup
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t wave = SOLO ? blockIdx.x & 3u : tid >> 6, sw = SOLO ? 0u : tid >> 6;
+    const uint32_t sw = SOLO ? 0u : tid >> 6;
     const uint64_t t_start = a.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
     // Tile of this block: heaviest-first order from the previous launch's
-    // measured per-tile cost when the host supplies one (tile_order), so the
-    // long tiles do not start last and form the launch's tail.
-    const uint32_t blk = SOLO ? blockIdx.x >> 2 : blockIdx.x;
-    const uint32_t tile = a.tile_order ? a.tile_order[blk] : blk;
+    // measured costs when the host supplies one (tile_order), so the long
+    // waves do not start last and form the launch's tail.  One-wave kernels
+    // rank waves (unit 4 * tile + quadrant), four-wave ones block tiles.
+    uint32_t tile, wave;
+    const bool unit_waves = SOLO && a.unit_waves != 0u;
+    if (unit_waves) {
+        const uint32_t u = a.tile_order ? a.tile_order[blockIdx.x] : blockIdx.x;
+        tile = u >> 2;
+        wave = u & 3u;
+    } else {
+        const uint32_t blk = SOLO ? blockIdx.x >> 2 : blockIdx.x;
+        tile = a.tile_order ? a.tile_order[blk] : blk;
+        wave = SOLO ? blockIdx.x & 3u : tid >> 6;
+    }
     const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
     const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t pl = lane / P, j = lane % P;  // pixel of the tile, sample lane of the pixel
@@ -985,6 +1001,14 @@ void trace_kernel(TraceArgs a) {
     const bool valid = x < a.width && ly < a.local_rows;
     const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
     const bool owner = j == 0;
+    // The running mean of a pixel is one sequential chain per colour channel, so
+    // with P >= 4 its lanes j = 0, 1, 2 each fold ONE channel (kept in accx) in
+    // lockstep: a fold step then costs one multiply and one add per lane, and a
+    // wave folds 3 chains per pixel at once (at P = 16 the owner's three-channel
+    // fold was ~15 % of the wave's VALU instructions).  The owner gathers the
+    // other two channels by DPP for the final store.
+    constexpr bool FOLD3 = RTK_FOLD3 != 0 && P >= 4;
+    const bool folder = FOLD3 ? j < 3u : owner;
     float4 *ring = s_ring + sw * kRing * kRingStride + pl;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
@@ -994,12 +1018,16 @@ void trace_kernel(TraceArgs a) {
     __syncthreads();
     const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
 
-    float accx = 0.0f, accy = 0.0f, accz = 0.0f;
-    if (valid && owner && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
+    float accx = 0.0f, accy = 0.0f, accz = 0.0f;  // FOLD3: accx = this folding lane's channel j
+    if (valid && folder && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
         const float4 pv = a.prev[(size_t)ly * a.width + x];
-        accx = pv.x;
-        accy = pv.y;
-        accz = pv.z;
+        if (FOLD3) {
+            accx = j == 0u ? pv.x : j == 1u ? pv.y : pv.z;
+        } else {
+            accx = pv.x;
+            accy = pv.y;
+            accz = pv.z;
+        }
     }
 
     // owner lanes of in-image pixels (they fold until every frame is folded)
@@ -1033,7 +1061,7 @@ void trace_kernel(TraceArgs a) {
         for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_mask[sw][w] == 0;
     if (empty_tile) {
         // (an all-zero running mean stays exactly zero: nothing to fold)
-        if (valid && owner && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
+        if (valid && folder && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
             for (uint32_t q = 0; q < a.frames; ++q) {
                 float ratio;
                 if (q < fold_n) {
@@ -1082,8 +1110,65 @@ void trace_kernel(TraceArgs a) {
                : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
                         : folded;
     };
+    // The pixel's parked frontier: every sample below it is in the ring.  A lane's
+    // samples below its cursor k are parked (mode 0: k not started yet; 1: k in
+    // flight; 2: k >= frames), so it is the minimum of k over the pixel's P lanes
+    // -- a DPP reduction inside the lane slice (quads, half rows, rows; a
+    // cross-row shuffle only for P = 32), run with every lane active.
+    auto parked_frontier = [&]() -> uint32_t {
+        uint32_t f = k;
+#define RTK_DMIN(CTRL) f = min(f, (uint32_t)__builtin_amdgcn_update_dpp((int)f, (int)f, CTRL, 0xf, 0xf, false))
+        if (P >= 2) RTK_DMIN(0xB1);   // quad_perm 1,0,3,2 (lane ^ 1)
+        if (P >= 4) RTK_DMIN(0x4E);   // quad_perm 2,3,0,1 (lane ^ 2)
+        if (P >= 8) RTK_DMIN(0x141);  // row_half_mirror (the other quad of the 8)
+        if (P >= 16) RTK_DMIN(0x140); // row_mirror (the other half of the row)
+#undef RTK_DMIN
+        if (P >= 32) f = min(f, (uint32_t)__shfl_xor((int)f, 16, 64));
+        return min(f, a.frames);
+    };
     auto fold_ring = [&]() {
-        if (P > 1 && owner && valid) {
+        if (RTK_FOLD_FRONTIER && P > 1) {
+            // ---- running-mean blend (main.cpp:484-489) of every parked sample, in
+            // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
+            // sample's lane.  Slots [folded, F) are all parked: no per-slot flags, no
+            // clearing writes.  Batches of four slots aligned to 4 (kRing is a multiple
+            // of 4, so a batch never wraps; its LDS reads take immediate offsets).
+            const uint32_t F = parked_frontier();
+            if (folder && valid) {
+                while (folded < F) {
+                    const uint32_t a0 = folded & ~3u;
+                    const float4 *base = ring + (a0 % kRing) * kRingStride;
+                    float v[4], w[4];
+                    float4 r4[4];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4u; ++i) {
+                        if (FOLD3) {  // this lane's channel j and the ratio
+                            const float *slot = reinterpret_cast<const float *>(base + i * kRingStride);
+                            v[i] = slot[j];
+                            w[i] = slot[3];
+                        } else {
+                            r4[i] = base[i * kRingStride];
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < 4u; ++i) {
+                        const bool take = a0 + i >= folded && a0 + i < F;
+                        if (FOLD3) {
+                            const float t = v[i] + accx * -w[i];
+                            accx = take ? t : accx;
+                        } else {
+                            const float tx = r4[i].x + accx * -r4[i].w;
+                            const float ty = r4[i].y + accy * -r4[i].w;
+                            const float tz = r4[i].z + accz * -r4[i].w;
+                            accx = take ? tx : accx;
+                            accy = take ? ty : accy;
+                            accz = take ? tz : accz;
+                        }
+                    }
+                    folded = min(a0 + 4u, F);
+                }
+            }
+        } else if (P > 1 && folder && valid) {
             // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
             // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
             // sample's lane.  The fold is one sequential chain per pixel, so the owner
@@ -1098,10 +1183,16 @@ void trace_kernel(TraceArgs a) {
                 for (uint32_t i = 0; i < kFoldBatch; ++i) {
                     more = more && folded < a.frames && __builtin_signbit(r[i].w);
                     if (more) {
-                        accx = r[i].x + accx * -r[i].w;
-                        accy = r[i].y + accy * -r[i].w;
-                        accz = r[i].z + accz * -r[i].w;
-                        ring[(folded % kRing) * kRingStride].w = 0.0f;
+                        if (FOLD3) {  // (lanes 1 and 2 read .w in this batch before lane 0 clears it)
+                            const float v = j == 0u ? r[i].x : j == 1u ? r[i].y : r[i].z;
+                            accx = v + accx * -r[i].w;
+                            if (owner) ring[(folded % kRing) * kRingStride].w = 0.0f;
+                        } else {
+                            accx = r[i].x + accx * -r[i].w;
+                            accy = r[i].y + accy * -r[i].w;
+                            accz = r[i].z + accz * -r[i].w;
+                            ring[(folded % kRing) * kRingStride].w = 0.0f;
+                        }
                         folded += 1u;
                     }
                 }
@@ -1298,6 +1389,10 @@ void trace_kernel(TraceArgs a) {
         if (kStats && a.stats) st_cyc_fold += __builtin_amdgcn_s_memtime() - st_t1;
     }
 
+    if (FOLD3) {  // channels 1 and 2 from lanes j = 1, 2 of the pixel's quad (quad_perm 1,1,1,1 / 2,2,2,2)
+        accy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(accx), 0x55, 0xf, 0xf, false));
+        accz = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(accx), 0xAA, 0xf, 0xf, false));
+    }
     if (valid && owner && a.frames > 0) {
         const size_t pix = (size_t)ly * a.width + x;
         a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
@@ -1308,7 +1403,11 @@ void trace_kernel(TraceArgs a) {
     if (lane == 0 && nrays) atomicAdd(a.rays, (unsigned long long)nrays);
     if (a.tile_cost && lane == 0) {
         const uint64_t c = __builtin_amdgcn_s_memtime() - t_cost0;
-        atomicMax(a.tile_cost + tile, (uint32_t)(c < 0xFFFFFFFFull ? c : 0xFFFFFFFFull));
+        const uint32_t c32 = (uint32_t)(c < 0xFFFFFFFFull ? c : 0xFFFFFFFFull);
+        if (unit_waves)
+            a.tile_cost[4u * tile + wave] = c32 | 1u;  // (>= 1: a launched wave never ranks with dead ones)
+        else
+            atomicMax(a.tile_cost + tile, c32);
     }
     if (a.wave_times && lane == 0) {
         const uint64_t wid = (uint64_t)tile * 4u + wave;
@@ -1417,7 +1516,11 @@ __global__ __launch_bounds__(256) void cull_kernel(TraceArgs a, uint32_t *live, 
     if (threadIdx.x == 0) {
         const bool l = s_any != 0 || !empty_capable;
         live[tile] = l ? 1u : 0u;
-        cost[tile] = l ? 2u : 0u;
+        if (a.unit_waves) {  // the one-wave kernels' order ranks waves (4 * tile + quadrant)
+            for (uint32_t w = 0; w < 4u; ++w) cost[4u * tile + w] = l ? 2u : 0u;
+        } else {
+            cost[tile] = l ? 2u : 0u;
+        }
         const uint32_t stripe = tile % kCullStripes;
         if (l) {
             atomicAdd(counters + stripe, 1ull);
