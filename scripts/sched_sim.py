@@ -69,3 +69,41 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def split_tail(durations, slots, x):
+    """The last x jobs (in order) split into two halves of half the duration;
+    the second halves go after everything else and may start only when their
+    first half has finished (a dispatched second half occupies its slot
+    while it waits)."""
+    d = list(durations)
+    n = len(d)
+    x = min(x, n)
+    jobs = [(di, None) for di in d[: n - x]] + [(di / 2.0, ("a", k)) for k, di in enumerate(d[n - x:])] + \
+           [(di / 2.0, ("b", k)) for k, di in enumerate(d[n - x:])]
+    free = [0.0] * min(slots, len(jobs))
+    heapq.heapify(free)
+    done_a = {}
+    end = 0.0
+    for dur, tag in jobs:
+        t = heapq.heappop(free)
+        start = t
+        if tag and tag[0] == "b":
+            start = max(t, done_a[tag[1]])
+        fin = start + dur
+        if tag and tag[0] == "a":
+            done_a[tag[1]] = fin
+        heapq.heappush(free, fin)
+        end = max(end, fin)
+    return end
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:
+    z = np.load(sys.argv[1])
+    wt = z["wave_times"].astype(np.int64)
+    live = wt[:, 1] > 0
+    du = (wt[live, 1] - wt[live, 0]) / 100.0
+    slots = 256 * 4 * 7
+    order = np.sort(du)[::-1]
+    for x in (0, 3584, 7168, 14336):
+        print(f"  wave_exact + split of the last {x:5d} waves: makespan {split_tail(order, slots, x):7.0f} us")
