@@ -296,10 +296,13 @@ def scene_clusters(scene: RtScene, simd: bool = True):
         _check(lib().rt_scene_clusters(ctypes.byref(scene), int(simd), tab.ctypes.data, nf4.value, ctypes.byref(nf4),
                                        ctypes.byref(ncp)), "rt_scene_clusters")
     # the pair-mask words follow the rule set's group count (rt_host.cpp pack_set):
-    # SIMDSpheres groups for the SIMD rules, ceil(ScalarSpheres / 4) for the scalar ones
+    # SIMDSpheres groups for the SIMD rules, ceil(ScalarSpheres / 4) for the scalar ones;
+    # per-lane ("relative") tables carry a fifth row at one word (the height slab)
     groups = scene.SIMDSpheres.Count if simd else (scene.ScalarSpheres.Count + 3) // 4
     words = 1 if groups <= 32 else 2 if groups <= 64 else 4
-    return tab.reshape(-1, 4 if words == 1 else 3 + words, 4), int(ncp.value)
+    relative = bool(scene_prefilter(scene, simd)[2] & 4)
+    rows = (5 if relative else 4) if words == 1 else 3 + words
+    return tab.reshape(-1, rows, 4), int(ncp.value)
 
 
 def rsqrt_table_builtin() -> np.ndarray:

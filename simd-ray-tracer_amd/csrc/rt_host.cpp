@@ -495,6 +495,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     struct Cl {
         float qx, qy, qz, t;
         float b;                    // behind threshold (below)
+        float srho = 0.0f, ymid = 0.0f, yhalf = INFINITY;  // height-slab bound (relative tables, below)
         std::vector<uint32_t> mem;  // sphere slots, ascending
     };
     std::vector<Cl> cl;
@@ -537,6 +538,30 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
             }
             C.t = std::nextafter((float)(rho * rho * (1.0 + a_rel) * (1.0 + 1e-6)), INFINITY);
             C.b = std::nextafter((float)(-(bmax + 4.3 * u) * (1.0 + 1e-6)), -INFINITY);
+            // Height slab.  A lane can accept member j only if its exact line passes
+            // within sigma_j = sqrt(r_j^2 + 13.3u |C_j|^2) <= r_j + k_s |C_j| of s_j
+            // (k_s = sqrt(13.3u) = 8.9e-4; the reference-rounded dist error, as above),
+            // so at some t with |O + tD - q_c| <= rho_s + k_s |C_j|, rho_s = max_j
+            // (delta_j + r_j), and height within [y_lo - k_s|C_j|, y_hi + k_s|C_j|]
+            // (y_lo/y_hi the members' extent).  Along the line the height O.y + t D.y
+            // over that t range lies within c +- |D.y| rho' (c = O.y + D.y T, T the
+            // projection of q_c): if |c - ymid| > yhalf + |D.y| rho' + E the line misses
+            // every member.  |C_j| <= |Q| + delta_j, |Q| <= (1 + cc)/2: the delta_j part
+            // is folded into srho / yhalf here, the |Q| part (twice, for height and t
+            // range) and the rounding of T, c, d and thr (< 2^-14 (1 + cc) + u |O.y|)
+            // into the kernel's per-lane E = cc kSlabRel + |O.y| 2^-21 + kSlabRel,
+            // kSlabRel = 2^-9 >= 2 (8.9e-4 (1.0001) / 2 + 2^-14).
+            double rs = 0.0, yhi = -INFINITY, ylo = INFINITY;
+            for (uint32_t i : C.mem) {
+                rs = std::max(rs, delta(i) + sp[i].r);
+                yhi = std::max(yhi, sp[i].y + sp[i].r);
+                ylo = std::min(ylo, sp[i].y - sp[i].r);
+            }
+            const double ks = 8.91e-4;
+            C.srho = std::nextafter((float)(rs * (1.0 + ks) * (1.0 + 0x1p-12)), INFINITY);
+            C.ymid = (float)((yhi + ylo) * 0.5);
+            const double half = std::max(yhi - (double)C.ymid, (double)C.ymid - ylo) + ks * rs;
+            C.yhalf = std::nextafter((float)(half * (1.0 + 0x1p-12)), INFINITY);
         } else {
             double rho = 0.0;
             for (uint32_t i : C.mem) rho = std::max(rho, delta(i) + sigma(sp[i]));
@@ -551,11 +576,11 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         for (uint32_t &i : C.mem) i = sp[i].s;
         cl.push_back(std::move(C));
     }
-    if (cl.size() & 1u) cl.push_back(Cl{0.0f, 0.0f, 0.0f, -INFINITY, 0.0f, {}});
+    if (cl.size() & 1u) cl.push_back(Cl{0.0f, 0.0f, 0.0f, -INFINITY, 0.0f, 0.0f, 0.0f, INFINITY, {}});
     const uint32_t n_cp = (uint32_t)cl.size() / 2u;
     uint32_t n_mp = 0;
     for (const Cl &C : cl) n_mp += ((uint32_t)C.mem.size() + 1u) / 2u;
-    const uint32_t ef = cl_entry_f4(*words) * 4u;  // floats per entry
+    const uint32_t ef = cl_entry_f4(*words, relative) * 4u;  // floats per entry
     tab.assign((size_t)(n_cp + n_mp) * ef, 0.0f);
     auto put_u = [&](size_t at, uint32_t v) { memcpy(&tab[at], &v, 4); };
     auto sphere_xyz = [&](uint32_t s, int axis) {
@@ -572,6 +597,10 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         const Cl &A = cl[2u * p], &B = cl[2u * p + 1u];
         e[0] = A.qx, e[1] = B.qx, e[2] = A.qy, e[3] = B.qy, e[4] = A.qz, e[5] = B.qz, e[6] = A.t, e[7] = B.t;
         e[12] = A.b, e[13] = B.b;
+        if (relative) {  // the height-slab bound (rt_kernel.h: row 3 zw, row 4)
+            e[14] = A.srho, e[15] = B.srho;
+            e[16] = A.ymid, e[17] = B.ymid, e[18] = A.yhalf, e[19] = B.yhalf;
+        }
         const Cl *two[2] = {&A, &B};
         for (int h = 0; h < 2; ++h) {
             const uint32_t cnt = ((uint32_t)two[h]->mem.size() + 1u) / 2u;

@@ -25,9 +25,15 @@ enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // entry holds that bit in the row of word q >> 6 and 0 in the others, so the kernel
 // merges a flagged member into every word with one select and one OR each.
 // With pf_relative the thresholds are per lane: rc2p / r2p hold R_c / r^2 and
-// b the M-free behind bases (rt_host.cpp cluster_table, "relative").
+// b the M-free behind bases (rt_host.cpp cluster_table, "relative"), and a
+// cluster pair also carries its height-slab bound (rt_kernel.hip slab test):
+//   row 3 = {b0 b1 srho0 srho1}, row 4 = {ymid0 ymid1 yhalf0 yhalf1}
+// (entries then have at least 5 rows; member entries leave row 4 to the bits).
 // padding members: threshold -inf, bits 0.
-constexpr uint32_t cl_entry_f4(uint32_t words) { return words == 1u ? 4u : 3u + words; }
+constexpr uint32_t cl_entry_f4(uint32_t words, bool relative = false) {
+    return words == 1u ? (relative ? 5u : 4u) : 3u + words;
+}
+constexpr float kSlabRel = 0x1p-9f;  // the slab test's per-lane margin per unit of cc (rt_host.cpp cluster_table)
 constexpr uint32_t kClMaxGroups = 128;   // table built up to this many groups
 constexpr uint32_t kClAutoGroups = 128;  // used by default up to this many (rt_host.cpp clusters_env; RTWeekend's
                                          // 121 groups: 11.3k Mrays/s clustered against 9.4k per group)

@@ -662,7 +662,7 @@ __device__ __forceinline__ void merge_words(uint64_t (&wave)[kClWords], uint64_t
 template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
                                              uint64_t (&wave)[kClWords], PfStats *ps) {
-    constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W);
+    constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W, REL);
     if (ps) ps->groups += count;
     const uint32_t end = (first + count) * kEntryBytes;
     for (uint32_t off = first * kEntryBytes; off != end; off += kEntryBytes) {
@@ -701,7 +701,10 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
                                                  Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
-    constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W);
+    constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W, REL);
+    // per-lane part of the height-slab margin (REL tables; rt_host.cpp cluster_table)
+    const float oy = ray.y.x, dy = ray.y.y;
+    const float slab_e0 = REL ? __builtin_fmaf(__builtin_fabsf(oy), 0x1p-21f, kSlabRel) : 0.0f;
     for (uint32_t off = 0, end = a.n_cpairs * kEntryBytes; off != end; off += kEntryBytes) {
         cv4f_t *e = cl_entry(ct, off);
         const v4f_t r0 = e[0], r1 = e[1];
@@ -712,8 +715,25 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         const float t1 = REL ? __builtin_fmaf(cc.y, kClRel, r1.w) : r1.w;
         const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-        const bool in0 = ballot_and(!(v.x >= t0), !(T.x < b0)) != 0;
-        const bool in1 = ballot_and(!(v.y >= t1), !(T.y < b1)) != 0;
+        uint64_t m0 = ballot_and(!(v.x >= t0), !(T.x < b0));
+        uint64_t m1 = ballot_and(!(v.y >= t1), !(T.y < b1));
+        if constexpr (REL) {
+            // Height slab: the line's height over the t range that can reach the
+            // cluster is c +- |D.y| srho with c = O.y + D.y T; it cannot meet a
+            // member when that range clears [ymid - yhalf, ymid + yhalf] by the
+            // lane's margin E (a ground-plane scene: rays leaving the ground cross the
+            // thin layer of small spheres only near their origin).
+            const v4f_t r4 = e[4];
+            const f2 E = __builtin_elementwise_fma(cc, f2{kSlabRel, kSlabRel}, f2{slab_e0, slab_e0});
+            const f2 c = __builtin_elementwise_fma(f2{dy, dy}, T, f2{oy, oy});
+            const f2 d = c - f2{r4.x, r4.y};
+            const f2 thr = __builtin_elementwise_fma(f2{__builtin_fabsf(dy), __builtin_fabsf(dy)}, f2{r3.z, r3.w},
+                                                     f2{r4.z, r4.w} + E);
+            m0 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
+            m1 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
+        }
+        const bool in0 = m0 != 0;
+        const bool in1 = m1 != 0;
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
         if (in0) member_pairs<W, REL>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
         if (in1) member_pairs<W, REL>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);

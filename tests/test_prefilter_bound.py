@@ -42,6 +42,20 @@ PF_REL = F(2.0 ** -15)  # rt_kernel.hip kPfRel
 
 CL_REL = F(9.2e-4)            # rt_kernel.hip kClRel
 BEHIND_REL = F(4.5 * 2.0 ** -24)  # rt_kernel.hip kBehindRel
+SLAB_REL = F(2.0 ** -9)       # rt_kernel.h kSlabRel
+
+
+def slab_skip(tc, cc, oy, dy, srho, ymid, yhalf):
+    """rt_kernel.hip clustered_groups, per-lane tables: the height-slab test skips a
+    cluster when |RN(fma(D.y, T, O.y)) - ymid| > RN(fma(|D.y|, srho, yhalf + E)),
+    E = RN(fma(cc, kSlabRel, RN(fma(|O.y|, 2^-21, kSlabRel))))."""
+    with np.errstate(invalid="ignore", over="ignore"):
+        e0 = fma(np.abs(oy), np.broadcast_to(F(2.0 ** -21), oy.shape), np.broadcast_to(SLAB_REL, oy.shape))
+        E = fma(cc, np.broadcast_to(SLAB_REL, cc.shape), e0)
+        c = fma(dy, tc, oy)
+        d = (c - F(ymid)).astype(F)
+        thr = fma(np.abs(dy), np.broadcast_to(F(srho), dy.shape), (F(yhalf) + E).astype(F))
+        return np.abs(d) > thr
 
 
 def cluster_threshold(t, cc, relative):
@@ -241,8 +255,9 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
                     used.add(s[0])
                     ms.append(s[0])
                     beta_of[s[0]] = np.float32(e[3][w])
+            slab = (np.float32(q[3][2 + h]), np.float32(q[4][h]), np.float32(q[4][2 + h])) if relative else None
             members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
-                            np.float32(q[1][2 + h]), ms, np.float32(q[3][h])))
+                            np.float32(q[1][2 + h]), ms, np.float32(q[3][h]), slab))
     covered = sorted(s for m in members for s in m[4])
     assert covered == sorted(np.flatnonzero(live)), "every hittable sphere is in exactly one cluster"
     rng = np.random.default_rng(seed)
@@ -263,8 +278,8 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
     assert not np.any(accept & skip_s), "the member test skipped a sphere a lane can accept"
     if require_culls:
         assert np.any((t_s < beta_s) & (e_s < thr_s) & live[None, :]), "the behind rule culls nothing"
-    skipped_any = behind_any = 0
-    for qx, qy, qz, t, ms, bc in members:
+    skipped_any = behind_any = slab_any = 0
+    for qx, qy, qz, t, ms, bc, slab in members:
         if np.isneginf(t):
             continue
         ex, tx, cq = prefilter((qx - o[:, 0])[:, None], (qy - o[:, 1])[:, None], (qz - o[:, 2])[:, None],
@@ -272,9 +287,15 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
         tc = cluster_threshold(t, cq[:, 0], relative)
         behind = tx[:, 0] < behind_threshold(bc, cq[:, 0], relative)
         skip = ~(ex[:, 0] < tc) | behind
+        if slab is not None:
+            sl = slab_skip(tx[:, 0], cq[:, 0], o[:, 1], d[:, 1], *slab)
+            slab_any += int((sl & ~skip).sum())
+            skip = skip | sl
         skipped_any += int(skip.sum())
         behind_any += int((behind & (ex[:, 0] < tc)).sum())
         assert not np.any(accept[skip][:, ms]), "a skipped cluster holds a sphere a lane can accept"
     if require_culls:
         assert skipped_any > 0 and behind_any > 0  # both cluster rules cull
+        if relative:
+            assert slab_any > 0, "the height-slab rule culls nothing"
     return skipped_any, behind_any
