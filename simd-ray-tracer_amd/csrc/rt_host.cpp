@@ -420,7 +420,10 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // max(1.25 sqrt(n), n/8) clusters: measured on C2 (N = 64) K = 6/8/10/12/16 ->
     // 112.4k/113.8k/114.6k/114.5k/111.4k Mrays/s; at 200 spheres K = 17/28 ->
     // 45.0k/46.9k; at C5 (256) K = 20/26/32/40 -> 30.1k/31.3k/32.4k/32.4k
-    uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / 8u));
+    // per-lane tables carry the height-slab test, which culls most clusters of a
+    // ground-plane scene, so fewer (larger) clusters pay there: RTWeekend (482
+    // spheres) K = 32/40/60/90 -> 17.8k/18.5k/17.8k/16.7k Mrays/s, hence n/12
+    uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / (relative ? 12u : 8u)));
     if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob
     // k-means (f64, fixed LCG restarts) minimising the sum of rho_c^2
     std::vector<uint32_t> best_lab;
