@@ -28,7 +28,7 @@ struct rt_device {
     bool use_sky = false;
     int src = kSrcSmem;
     int cull = 1;
-    uint32_t sec_threshold = 16;
+    uint32_t sec_threshold = 0;  // 0: per scene (rt_trace), else RT_SEC_THRESHOLD
     int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
     uint32_t pf_relative[2] = {0, 0};  // per rule set: row 3 holds r^2, per-lane thresholds (rt_kernel.hip kPfRel)
@@ -851,7 +851,6 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.band_rows = band_rows;
     a.band_count = band_count;
     a.band_index = desc->BandIndex;
-    a.sec_threshold = d->sec_threshold;
     a.prefilter = d->prefilter[rs];
     a.pf_relative = d->pf_relative[rs];
     a.fast_sqrt = d->fast_sqrt[rs];
@@ -861,6 +860,13 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         a.n_cpairs = d->n_cpairs[rs];
         a.cl_words = d->cl_words[rs];
     }
+    // Lanes that must wait before a secondary round runs: the dearer a wave's
+    // secondary round (cluster pairs, or groups without clusters), the more it
+    // pays to fill it first.  Measured (same box, Mrays/s, threshold 16/32/40/48):
+    // RTWeekend (20 cluster pairs) 18.6k/19.4k/19.5k/19.5k, C5 at 512 spp (16)
+    // 44.7k/46.3k/46.4k/46.4k, C2 (5) 153.8k/151.2k/150.4k/149.9k.
+    a.sec_threshold = d->sec_threshold;
+    if (a.sec_threshold == 0) a.sec_threshold = (a.clusters ? a.n_cpairs : a.n_groups) >= 12u ? 40u : 16u;
     a.stats = d->d_stats;
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
