@@ -224,6 +224,59 @@ def test_on_render_progressive_driver(rt, orc, torch_cuda):
     rt.on_shutdown()
 
 
+def test_on_render_busy_poll_hands_out_every_frame_in_order(rt, orc, torch_cuda):
+    """The platform loop without waits (bench.py --config onrender): calls that
+    find the frame still tracing return 0; every completed frame handed out is
+    the progressive mean over one more frame, while the next one already traces
+    in the other device slot."""
+    rt.on_init()
+    try:
+        W, H = 64, 48
+        img = np.zeros((H, W), np.uint32)
+        o = orc.scene_builtin(1)
+        ocam = orc.camera(o, W, H)
+        rt.on_render(img, 1)
+        got = []
+        for _ in range(200000):
+            done, rays, _ = rt.on_render(img, 1)
+            if done:
+                got.append((img.copy(), rays))
+                if len(got) == 4:
+                    break
+        assert len(got) == 4
+        for k, (im, rays) in enumerate(got):
+            _, ocur, orays = orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5)
+            assert np.array_equal(im.reshape(-1), ocur), k
+        rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
+
+
+def test_on_render_moving_camera_restarts_every_frame(rt, orc, torch_cuda):
+    """RT_KEY_LEFT on every call (main.cpp:743-746): each call turns the camera
+    by 1/16 rad, restarts the mean, and hands out the previous call's frame --
+    one frame under the previous call's camera."""
+    rt.on_init()
+    try:
+        W, H = 56, 40
+        img = np.zeros((H, W), np.uint32)
+        o = orc.scene_builtin(2)
+        angle = np.float32(o.x_angle)
+        angles = []
+        for j in range(4):
+            angle = np.float32(angle + np.float32(1.0 / 16.0))  # the key's f32 step
+            angles.append(angle)
+            done, _, _ = rt.on_render(img, 2, keys=rt.KEY_LEFT)
+            assert done == (j > 0)
+            if j > 0:
+                ocam = orc.camera(o, W, H, x_angle=float(angles[j - 1]))
+                _, ocur, _ = orc.render(o, ocam, W, H, frames=1, max_bounce=5)
+                assert np.array_equal(img.reshape(-1), ocur), j
+        rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
+
+
 # Kernel variants selected at device creation (rt_host.cpp reads the env):
 # prefilter forced on/off, brute-force primaries, 1/2/16/32 lanes per pixel, the
 # LDS-staged sphere source, four-wave workgroups, the run-time walk dispatch.
