@@ -887,6 +887,9 @@ constexpr uint32_t kFoldTable = 256;
 #ifndef RTK_FOLD_FRONTIER  // 1: ring readiness from the lanes' sample cursors, not per-slot flags (A/B)
 #define RTK_FOLD_FRONTIER 1
 #endif
+#ifndef RTK_FOLD_WHOLE  // 1: the frontier fold takes whole aligned batches of four, no per-slot selects (A/B)
+#define RTK_FOLD_WHOLE 1
+#endif
 #ifndef RTK_FOLD_BATCH_SMALL_P  // ring slots the owner reads per LDS round trip at P <= 4 (A/B)
 #define RTK_FOLD_BATCH_SMALL_P 2
 #endif
@@ -1029,6 +1032,11 @@ void trace_kernel(TraceArgs a) {
     // other two channels by DPP for the final store.
     constexpr bool FOLD3 = RTK_FOLD3 != 0 && P >= 4;
     const bool folder = FOLD3 ? j < 3u : owner;
+    // the channel a lane reads from a ring slot (lanes j >= 3 of the whole-batch fold
+    // read the ratio word and discard their sums)
+    const uint32_t jc = j < 3u ? j : 3u;
+    // every lane of a pixel keeps the fold cursor (whole-batch frontier fold)
+    constexpr bool kCursorPerLane = RTK_FOLD_FRONTIER && RTK_FOLD_WHOLE && P > 1;
     float4 *ring = s_ring + sw * kRing * kRingStride + pl;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
@@ -1125,7 +1133,8 @@ void trace_kernel(TraceArgs a) {
     };
     // the pixel's owner lane's fold cursor (first of its P-lane slice) via DPP
     auto fold_cursor = [&]() -> uint32_t {
-        return P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
+        return kCursorPerLane ? folded
+               : P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
                : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
                : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
                         : folded;
@@ -1154,7 +1163,55 @@ void trace_kernel(TraceArgs a) {
             // clearing writes.  Batches of four slots aligned to 4 (kRing is a multiple
             // of 4, so a batch never wraps; its LDS reads take immediate offsets).
             const uint32_t F = parked_frontier();
-            if (folder && valid) {
+            if (RTK_FOLD_WHOLE && valid) {
+                // Whole aligned batches only (folded stays a multiple of 4), each slot
+                // folded straight with no per-slot test; the ragged end once every
+                // sample is parked.  A lane that waits for ring space still gets it: the
+                // lane holding the frontier sample F < folded + 4 <= folded + kRing
+                // is never blocked, so the frontier keeps moving.  Every lane of the
+                // pixel runs the loop (F is uniform over them), so each keeps the fold
+                // cursor itself; only the folding lanes' sums are used.
+                const uint32_t Fb = F >= a.frames ? F : (F & ~3u);
+                while (folded + 4u <= Fb) {
+                    const float4 *base = ring + (folded % kRing) * kRingStride;
+                    float v[4], w[4];
+                    float4 r4[4];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4u; ++i) {
+                        if (FOLD3) {
+                            const float *slot = reinterpret_cast<const float *>(base + i * kRingStride);
+                            v[i] = slot[jc];
+                            w[i] = slot[3];
+                        } else {
+                            r4[i] = base[i * kRingStride];
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < 4u; ++i) {
+                        if (FOLD3) {
+                            accx = v[i] + accx * -w[i];
+                        } else {
+                            accx = r4[i].x + accx * -r4[i].w;
+                            accy = r4[i].y + accy * -r4[i].w;
+                            accz = r4[i].z + accz * -r4[i].w;
+                        }
+                    }
+                    folded += 4u;
+                }
+                while (folded < Fb) {
+                    const float4 *s4 = ring + (folded % kRing) * kRingStride;
+                    if (FOLD3) {
+                        const float *slot = reinterpret_cast<const float *>(s4);
+                        accx = slot[jc] + accx * -slot[3];
+                    } else {
+                        const float4 r = *s4;
+                        accx = r.x + accx * -r.w;
+                        accy = r.y + accy * -r.w;
+                        accz = r.z + accz * -r.w;
+                    }
+                    folded += 1u;
+                }
+            } else if (folder && valid) {
                 while (folded < F) {
                     const uint32_t a0 = folded & ~3u;
                     const float4 *base = ring + (a0 % kRing) * kRingStride;
