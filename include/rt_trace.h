@@ -400,6 +400,12 @@ int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r
  * against it on the CPU (tests/test_prefilter_bound.py). */
 int rt_scene_clusters(const rt_scene *scene, uint32_t enable_simd, float *out, uint32_t capacity_f4,
                       uint32_t *out_f4, uint32_t *out_cpairs);
+/* The table's levels (test/inspection hook): *out_levels = 1 (cluster-pair
+ * entries index member entries), 2 (tables of two or more pair-mask words: the
+ * *out_cpairs top entries index *out_sub_pairs sub-cluster pair entries, which
+ * index the member entries) or 0 (no table). */
+int rt_scene_cluster_layout(const rt_scene *scene, uint32_t enable_simd, uint32_t *out_levels,
+                            uint32_t *out_sub_pairs);
 const char *rt_last_error(void);
 
 /* ----------------------------------------------- OnInit / OnRender driver */

@@ -151,6 +151,7 @@ SIGNATURES = {
                                    POINTER(c_uint32)]),
     "rt_scene_clusters": (c_int, [POINTER(RtScene), c_uint32, c_void_p, c_uint32, POINTER(c_uint32),
                                   POINTER(c_uint32)]),
+    "rt_scene_cluster_layout": (c_int, [POINTER(RtScene), c_uint32, POINTER(c_uint32), POINTER(c_uint32)]),
     "rt_last_error": (c_char_p, []),
     "rt_on_init": (c_int, [POINTER(RtInitParams)]),
     "rt_on_init_devices": (c_int, [POINTER(RtInitParams), POINTER(c_int), c_uint32]),
@@ -303,6 +304,16 @@ def scene_clusters(scene: RtScene, simd: bool = True):
     relative = bool(scene_prefilter(scene, simd)[2] & 4)
     rows = (5 if relative else 4) if words == 1 else 3 + words
     return tab.reshape(-1, rows, 4), int(ncp.value)
+
+
+def scene_cluster_layout(scene: RtScene, simd: bool = True):
+    """(levels, sub_pairs) of the clustered prefilter table (rt_scene_cluster_layout):
+    levels 2 means the first n_cpairs entries index sub_pairs sub-cluster pair
+    entries, which index the member entries."""
+    lv, sp = c_uint32(), c_uint32()
+    _check(lib().rt_scene_cluster_layout(ctypes.byref(scene), int(simd), ctypes.byref(lv), ctypes.byref(sp)),
+           "rt_scene_cluster_layout")
+    return int(lv.value), int(sp.value)
 
 
 def rsqrt_table_builtin() -> np.ndarray:

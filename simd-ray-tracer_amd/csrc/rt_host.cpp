@@ -385,7 +385,10 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
 //   member   -(r_j (1 + 2^-15) + 4.3u),
 // and a lane's behind test is T < RN(stored - 4.5u cc).
 static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, std::vector<float> &tab,
-                              uint32_t *words, bool relative = false) {
+                              uint32_t *words, bool relative = false, uint32_t *levels = nullptr,
+                              uint32_t *sub_pairs = nullptr) {
+    if (levels) *levels = 0;
+    if (sub_pairs) *sub_pairs = 0;
     tab.clear();
     *words = n_groups <= 32u ? 1u : n_groups <= 64u ? 2u : 4u;
     if (n_groups > kClMaxGroups) return 0;
@@ -423,77 +426,93 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // per-lane tables carry the height-slab test, which culls most clusters of a
     // ground-plane scene, so fewer (larger) clusters pay there: RTWeekend (482
     // spheres) K = 32/40/60/90 -> 17.8k/18.5k/17.8k/16.7k Mrays/s, hence n/12
-    uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / (relative ? 12u : 8u)));
+    // Two-level tables (two or more mask words, below) take fewer, larger top
+    // clusters over sub-clusters of 3 (scene-wide) or 4 (per-lane) spheres:
+    // RTWeekend K/S = 40/4, 28/3, 28/4, 24/4 -> 21.1k/21.9k/21.9k/21.7k (one level
+    // at K 40: 19.6k); C5 at 512 spp K/S = 32/4, 24/3, 28/3, 24/2 -> 47.4k/48.2k/
+    // 48.3k/48.3k (one level: 46.3k).
+    const bool two_levels = *words >= 2u;
+    const uint32_t div = two_levels ? (relative ? 17u : 10u) : (relative ? 12u : 8u);
+    uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / div));
     if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob
-    // k-means (f64, fixed LCG restarts) minimising the sum of rho_c^2
-    std::vector<uint32_t> best_lab;
-    double best_cost = INFINITY;
+    // k-means (f64, fixed LCG restarts) of the spheres idx into k clusters,
+    // minimising the sum of rho_c^2; returns each sphere's label
     uint64_t lcg = 0x9E3779B97F4A7C15ull;
     auto rnd = [&](uint32_t m) {
         lcg = lcg * 6364136223846793005ull + 1442695040888963407ull;
         return (uint32_t)((lcg >> 33) % m);
     };
-    std::vector<double> cx(k), cy(k), cz(k);
-    std::vector<uint32_t> lab(n);
-    for (int restart = 0; restart < 16; ++restart) {
-        for (uint32_t c = 0; c < k; ++c) {  // k-means++ style seeding (farthest of a few random picks)
-            uint32_t pick = rnd(n);
-            double far = -1.0;
-            for (int t = 0; t < 4 && c > 0; ++t) {
-                const uint32_t cand = rnd(n);
-                double dmin = INFINITY;
-                for (uint32_t q = 0; q < c; ++q)
-                    dmin = std::min(dmin, (sp[cand].x - cx[q]) * (sp[cand].x - cx[q]) + (sp[cand].y - cy[q]) * (sp[cand].y - cy[q]) +
-                                              (sp[cand].z - cz[q]) * (sp[cand].z - cz[q]));
-                if (dmin > far) {
-                    far = dmin;
-                    pick = cand;
-                }
-            }
-            cx[c] = sp[pick].x;
-            cy[c] = sp[pick].y;
-            cz[c] = sp[pick].z;
-        }
-        for (int it = 0; it < 40; ++it) {
-            for (uint32_t i = 0; i < n; ++i) {
-                double dmin = INFINITY;
-                for (uint32_t c = 0; c < k; ++c) {
-                    const double d2 = (sp[i].x - cx[c]) * (sp[i].x - cx[c]) + (sp[i].y - cy[c]) * (sp[i].y - cy[c]) +
-                                      (sp[i].z - cz[c]) * (sp[i].z - cz[c]);
-                    if (d2 < dmin) {
-                        dmin = d2;
-                        lab[i] = c;
+    auto kmeans = [&](const std::vector<uint32_t> &idx, uint32_t k, int restarts) {
+        const uint32_t m = (uint32_t)idx.size();
+        std::vector<uint32_t> best_lab(m, 0u);
+        double best_cost = INFINITY;
+        std::vector<double> cx(k), cy(k), cz(k);
+        std::vector<uint32_t> lab(m);
+        for (int restart = 0; restart < restarts; ++restart) {
+            for (uint32_t c = 0; c < k; ++c) {  // k-means++ style seeding (farthest of a few random picks)
+                uint32_t pick = rnd(m);
+                double far = -1.0;
+                for (int t = 0; t < 4 && c > 0; ++t) {
+                    const uint32_t cand = rnd(m);
+                    const Sph &o = sp[idx[cand]];
+                    double dmin = INFINITY;
+                    for (uint32_t q = 0; q < c; ++q)
+                        dmin = std::min(dmin, (o.x - cx[q]) * (o.x - cx[q]) + (o.y - cy[q]) * (o.y - cy[q]) +
+                                                  (o.z - cz[q]) * (o.z - cz[q]));
+                    if (dmin > far) {
+                        far = dmin;
+                        pick = cand;
                     }
                 }
+                const Sph &o = sp[idx[pick]];
+                cx[c] = o.x;
+                cy[c] = o.y;
+                cz[c] = o.z;
             }
-            std::vector<double> sx(k, 0.0), sy(k, 0.0), sz(k, 0.0), cnt(k, 0.0);
-            for (uint32_t i = 0; i < n; ++i) {
-                sx[lab[i]] += sp[i].x;
-                sy[lab[i]] += sp[i].y;
-                sz[lab[i]] += sp[i].z;
-                cnt[lab[i]] += 1.0;
-            }
-            for (uint32_t c = 0; c < k; ++c)
-                if (cnt[c] > 0.0) {
-                    cx[c] = sx[c] / cnt[c];
-                    cy[c] = sy[c] / cnt[c];
-                    cz[c] = sz[c] / cnt[c];
+            for (int it = 0; it < 40; ++it) {
+                for (uint32_t i = 0; i < m; ++i) {
+                    const Sph &o = sp[idx[i]];
+                    double dmin = INFINITY;
+                    for (uint32_t c = 0; c < k; ++c) {
+                        const double d2 = (o.x - cx[c]) * (o.x - cx[c]) + (o.y - cy[c]) * (o.y - cy[c]) +
+                                          (o.z - cz[c]) * (o.z - cz[c]);
+                        if (d2 < dmin) {
+                            dmin = d2;
+                            lab[i] = c;
+                        }
+                    }
                 }
+                std::vector<double> sx(k, 0.0), sy(k, 0.0), sz(k, 0.0), cnt(k, 0.0);
+                for (uint32_t i = 0; i < m; ++i) {
+                    sx[lab[i]] += sp[idx[i]].x;
+                    sy[lab[i]] += sp[idx[i]].y;
+                    sz[lab[i]] += sp[idx[i]].z;
+                    cnt[lab[i]] += 1.0;
+                }
+                for (uint32_t c = 0; c < k; ++c)
+                    if (cnt[c] > 0.0) {
+                        cx[c] = sx[c] / cnt[c];
+                        cy[c] = sy[c] / cnt[c];
+                        cz[c] = sz[c] / cnt[c];
+                    }
+            }
+            std::vector<double> rho(k, 0.0);
+            for (uint32_t i = 0; i < m; ++i) {
+                const Sph &o = sp[idx[i]];
+                const uint32_t c = lab[i];
+                const double d = std::sqrt((o.x - cx[c]) * (o.x - cx[c]) + (o.y - cy[c]) * (o.y - cy[c]) +
+                                           (o.z - cz[c]) * (o.z - cz[c]));
+                rho[c] = std::max(rho[c], d + sigma(o));
+            }
+            double cost = 0.0;
+            for (uint32_t c = 0; c < k; ++c) cost += rho[c] * rho[c];
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_lab = lab;
+            }
         }
-        std::vector<double> rho(k, 0.0);
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t c = lab[i];
-            const double d = std::sqrt((sp[i].x - cx[c]) * (sp[i].x - cx[c]) + (sp[i].y - cy[c]) * (sp[i].y - cy[c]) +
-                                       (sp[i].z - cz[c]) * (sp[i].z - cz[c]));
-            rho[c] = std::max(rho[c], d + sigma(sp[i]));
-        }
-        double cost = 0.0;
-        for (uint32_t c = 0; c < k; ++c) cost += rho[c] * rho[c];
-        if (cost < best_cost) {
-            best_cost = cost;
-            best_lab = lab;
-        }
-    }
+        return best_lab;
+    };
     // final clusters: f32 centres (what the kernel subtracts), exact thresholds
     struct Cl {
         float qx, qy, qz, t;
@@ -501,7 +520,6 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         float srho = 0.0f, ymid = 0.0f, yhalf = INFINITY;  // height-slab bound (relative tables, below)
         std::vector<uint32_t> mem;  // sphere slots, ascending
     };
-    std::vector<Cl> cl;
     // Behind thresholds: a member j cannot be accepted by a ray whose computed
     // T_j + X_j stays below eps (it = T - X or T + X < eps), and X_j <= r_j(1+2u).
     // With T_j within 4.2u sqrt(M_j)|D| of (S_j - O).D (one rounding in C_j, three
@@ -514,20 +532,19 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     for (const Sph &o : sp)
         beta_of_slot[o.s] = relative ? std::nextafter((float)(-(o.r * (1.0 + 0x1p-15) + 4.3 * u) * (1.0 + 1e-6)), -INFINITY)
                                      : std::nextafter((float)-(o.r * (1.0 + 0x1p-15) + 8.6 * u * std::sqrt(o.m)), -INFINITY);
-    for (uint32_t c = 0; c < k; ++c) {
+    // The bound rows of a cluster over the spheres idx (any set: a top cluster's
+    // bound covers every sphere under it, as a sub-cluster's covers its members).
+    auto make_cl = [&](const std::vector<uint32_t> &idx) {
         Cl C;
         double sx = 0.0, sy = 0.0, sz = 0.0;
-        for (uint32_t i = 0; i < n; ++i)
-            if (best_lab[i] == c) {
-                C.mem.push_back(i);
-                sx += sp[i].x;
-                sy += sp[i].y;
-                sz += sp[i].z;
-            }
-        if (C.mem.empty()) continue;
-        C.qx = (float)(sx / C.mem.size());
-        C.qy = (float)(sy / C.mem.size());
-        C.qz = (float)(sz / C.mem.size());
+        for (uint32_t i : idx) {
+            sx += sp[i].x;
+            sy += sp[i].y;
+            sz += sp[i].z;
+        }
+        C.qx = (float)(sx / idx.size());
+        C.qy = (float)(sy / idx.size());
+        C.qz = (float)(sz / idx.size());
         const double qx = C.qx, qy = C.qy, qz = C.qz;
         auto delta = [&](uint32_t i) {
             return std::sqrt((sp[i].x - qx) * (sp[i].x - qx) + (sp[i].y - qy) * (sp[i].y - qy) +
@@ -535,7 +552,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
         };
         if (relative) {
             double rho = 0.0, bmax = 0.0;
-            for (uint32_t i : C.mem) {
+            for (uint32_t i : idx) {
                 rho = std::max(rho, delta(i) * (1.0 + s_rel) + sp[i].r);
                 bmax = std::max(bmax, (delta(i) + sp[i].r) * (1.0 + 0x1p-15) + 4.3 * u * delta(i));
             }
@@ -555,7 +572,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
             // into the kernel's per-lane E = cc kSlabRel + |O.y| 2^-21 + kSlabRel,
             // kSlabRel = 2^-9 >= 2 (8.9e-4 (1.0001) / 2 + 2^-14).
             double rs = 0.0, yhi = -INFINITY, ylo = INFINITY;
-            for (uint32_t i : C.mem) {
+            for (uint32_t i : idx) {
                 rs = std::max(rs, delta(i) + sp[i].r);
                 yhi = std::max(yhi, sp[i].y + sp[i].r);
                 ylo = std::min(ylo, sp[i].y - sp[i].r);
@@ -567,24 +584,72 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
             C.yhalf = std::nextafter((float)(half * (1.0 + 0x1p-12)), INFINITY);
         } else {
             double rho = 0.0;
-            for (uint32_t i : C.mem) rho = std::max(rho, delta(i) + sigma(sp[i]));
+            for (uint32_t i : idx) rho = std::max(rho, delta(i) + sigma(sp[i]));
             const double mc = bound_m(qx, qy, qz);
             rho = (rho + u * std::sqrt(mc)) * (1.0 + 1e-6);
             C.t = std::nextafter((float)(rho * rho + mc * (32.0 * u + 1.01 * K)), INFINITY);
             double bmax = 0.0;
-            for (uint32_t i : C.mem)
+            for (uint32_t i : idx)
                 bmax = std::max(bmax, (delta(i) + sp[i].r) * (1.0 + 0x1p-15) + 4.3 * u * (std::sqrt(mc) + std::sqrt(sp[i].m)));
             C.b = std::nextafter((float)-bmax, -INFINITY);
         }
-        for (uint32_t &i : C.mem) i = sp[i].s;
-        cl.push_back(std::move(C));
+        for (uint32_t i : idx) C.mem.push_back(sp[i].s);
+        return C;
+    };
+    const Cl pad_cl{0.0f, 0.0f, 0.0f, -INFINITY, 0.0f, 0.0f, 0.0f, INFINITY, {}};  // never entered
+    // top clusters
+    std::vector<uint32_t> all(n);
+    for (uint32_t i = 0; i < n; ++i) all[i] = i;
+    const std::vector<uint32_t> top_lab = kmeans(all, k, 16);
+    std::vector<std::vector<uint32_t>> tops;
+    for (uint32_t c = 0; c < k; ++c) {
+        std::vector<uint32_t> idx;
+        for (uint32_t i = 0; i < n; ++i)
+            if (top_lab[i] == c) idx.push_back(i);
+        if (!idx.empty()) tops.push_back(std::move(idx));
     }
-    if (cl.size() & 1u) cl.push_back(Cl{0.0f, 0.0f, 0.0f, -INFINITY, 0.0f, 0.0f, 0.0f, INFINITY, {}});
+    std::vector<Cl> cl;
+    for (const auto &idx : tops) cl.push_back(make_cl(idx));
+    if (cl.size() & 1u) cl.push_back(pad_cl);
+    // Second level (tables of two or more mask words): each top cluster's spheres
+    // in sub-clusters of about kSubSpheres (k-means inside the top cluster), their
+    // pair entries contiguous per top cluster, padded to whole pairs.
+    const bool two = two_levels;
+    uint32_t sub_spheres = relative ? 4u : 3u;
+    if (const char *es = getenv("RT_SUB_SPHERES")) sub_spheres = std::max(1u, (uint32_t)atoi(es));  // A/B knob
+    std::vector<std::vector<Cl>> sub(cl.size());
+    if (two)
+        for (size_t c = 0; c < tops.size(); ++c) {
+            const std::vector<uint32_t> &idx = tops[c];
+            const uint32_t k2 = std::min((uint32_t)idx.size(), ((uint32_t)idx.size() + sub_spheres - 1u) / sub_spheres);
+            if (k2 <= 1u) {
+                sub[c].push_back(make_cl(idx));
+            } else {
+                const std::vector<uint32_t> lab = kmeans(idx, k2, 8);
+                for (uint32_t q = 0; q < k2; ++q) {
+                    std::vector<uint32_t> part;
+                    for (size_t i = 0; i < idx.size(); ++i)
+                        if (lab[i] == q) part.push_back(idx[i]);
+                    if (!part.empty()) sub[c].push_back(make_cl(part));
+                }
+            }
+            if (sub[c].size() & 1u) sub[c].push_back(pad_cl);
+        }
+    for (Cl &C : cl) std::sort(C.mem.begin(), C.mem.end());
+    for (auto &v : sub)
+        for (Cl &C : v) std::sort(C.mem.begin(), C.mem.end());
     const uint32_t n_cp = (uint32_t)cl.size() / 2u;
-    uint32_t n_mp = 0;
-    for (const Cl &C : cl) n_mp += ((uint32_t)C.mem.size() + 1u) / 2u;
+    uint32_t n_sp = 0, n_mp = 0;
+    for (size_t c = 0; c < cl.size(); ++c) {
+        if (two) {
+            n_sp += (uint32_t)sub[c].size() / 2u;
+            for (const Cl &S : sub[c]) n_mp += ((uint32_t)S.mem.size() + 1u) / 2u;
+        } else {
+            n_mp += ((uint32_t)cl[c].mem.size() + 1u) / 2u;
+        }
+    }
     const uint32_t ef = cl_entry_f4(*words, relative) * 4u;  // floats per entry
-    tab.assign((size_t)(n_cp + n_mp) * ef, 0.0f);
+    tab.assign((size_t)(n_cp + n_sp + n_mp) * ef, 0.0f);
     auto put_u = [&](size_t at, uint32_t v) { memcpy(&tab[at], &v, 4); };
     auto sphere_xyz = [&](uint32_t s, int axis) {
         const uint32_t g = (s / 4u) * 4u * kGroupF4, l = s % 4u;
@@ -594,47 +659,72 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     auto sphere_r2p = [&](uint32_t s) {
         return gv[(s / 4u) * 4u * kGroupF4 + 4u * (relative ? kRowR2 : kRowR2P) + s % 4u];
     };
-    uint32_t next = n_cp;
-    for (uint32_t p = 0; p < n_cp; ++p) {
+    // the bound rows of a cluster pair entry (both levels)
+    auto put_pair = [&](uint32_t p, const Cl &A, const Cl &B) {
         float *e = &tab[(size_t)p * ef];
-        const Cl &A = cl[2u * p], &B = cl[2u * p + 1u];
         e[0] = A.qx, e[1] = B.qx, e[2] = A.qy, e[3] = B.qy, e[4] = A.qz, e[5] = B.qz, e[6] = A.t, e[7] = B.t;
         e[12] = A.b, e[13] = B.b;
         if (relative) {  // the height-slab bound (rt_kernel.h: row 3 zw, row 4)
             e[14] = A.srho, e[15] = B.srho;
             e[16] = A.ymid, e[17] = B.ymid, e[18] = A.yhalf, e[19] = B.yhalf;
         }
-        const Cl *two[2] = {&A, &B};
+    };
+    uint32_t next_sub = n_cp, next = n_cp + n_sp;
+    // the member pair entries of cluster C from entry `next` on; returns their count
+    auto put_members = [&](const Cl &C) {
+        const uint32_t cnt = ((uint32_t)C.mem.size() + 1u) / 2u;
+        for (uint32_t q = 0; q < cnt; ++q, ++next) {
+            float *m = &tab[(size_t)next * ef];
+            const size_t mb = (size_t)next * ef;
+            for (int w = 0; w < 2; ++w) {
+                const uint32_t idx = 2u * q + (uint32_t)w;
+                if (idx < C.mem.size()) {
+                    const uint32_t s = C.mem[idx];
+                    m[0 + w] = sphere_xyz(s, kRowX);
+                    m[2 + w] = sphere_xyz(s, kRowY);
+                    m[4 + w] = sphere_xyz(s, kRowZ);
+                    m[6 + w] = sphere_r2p(s);
+                    m[12 + w] = beta_of_slot[s];
+                    // the u64 bit of pair q = s >> 1 in the row of word q >> 6 (row 2
+                    // for word 0, row 3 + w for word w >= 1; the other words' rows stay 0)
+                    const uint64_t bit = 1ull << ((s >> 1) & 63u);
+                    const uint32_t word = (s >> 1) >> 6;
+                    const size_t row = word == 0u ? 8u : 4u * (3u + word);
+                    put_u(mb + row + 2u * w, (uint32_t)bit);
+                    put_u(mb + row + 1u + 2u * w, (uint32_t)(bit >> 32));
+                } else {
+                    m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
+                }
+            }
+        }
+        return cnt;
+    };
+    for (uint32_t p = 0; p < n_cp; ++p) {
+        put_pair(p, cl[2u * p], cl[2u * p + 1u]);
         for (int h = 0; h < 2; ++h) {
-            const uint32_t cnt = ((uint32_t)two[h]->mem.size() + 1u) / 2u;
-            put_u((size_t)p * ef + 8u + 2u * h, next);
+            const size_t c = 2u * p + (uint32_t)h;
+            if (!two) {
+                put_u((size_t)p * ef + 8u + 2u * h, next);
+                put_u((size_t)p * ef + 9u + 2u * h, put_members(cl[c]));
+                continue;
+            }
+            // a top cluster: its sub-cluster pair entries, then their members
+            const uint32_t first = next_sub, cnt = (uint32_t)sub[c].size() / 2u;
+            put_u((size_t)p * ef + 8u + 2u * h, first);
             put_u((size_t)p * ef + 9u + 2u * h, cnt);
-            for (uint32_t q = 0; q < cnt; ++q, ++next) {
-                float *m = &tab[(size_t)next * ef];
-                const size_t mb = (size_t)next * ef;
-                for (int w = 0; w < 2; ++w) {
-                    const uint32_t idx = 2u * q + (uint32_t)w;
-                    if (idx < two[h]->mem.size()) {
-                        const uint32_t s = two[h]->mem[idx];
-                        m[0 + w] = sphere_xyz(s, kRowX);
-                        m[2 + w] = sphere_xyz(s, kRowY);
-                        m[4 + w] = sphere_xyz(s, kRowZ);
-                        m[6 + w] = sphere_r2p(s);
-                        m[12 + w] = beta_of_slot[s];
-                        // the u64 bit of pair q = s >> 1 in the row of word q >> 6 (row 2
-                        // for word 0, row 3 + w for word w >= 1; the other words' rows stay 0)
-                        const uint64_t bit = 1ull << ((s >> 1) & 63u);
-                        const uint32_t word = (s >> 1) >> 6;
-                        const size_t row = word == 0u ? 8u : 4u * (3u + word);
-                        put_u(mb + row + 2u * w, (uint32_t)bit);
-                        put_u(mb + row + 1u + 2u * w, (uint32_t)(bit >> 32));
-                    } else {
-                        m[6 + w] = -INFINITY;  // padding member: never flagged, no bit
-                    }
+            next_sub += cnt;
+            for (uint32_t q = 0; q < cnt; ++q) {
+                const uint32_t e = first + q;
+                put_pair(e, sub[c][2u * q], sub[c][2u * q + 1u]);
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    put_u((size_t)e * ef + 8u + 2u * h2, next);
+                    put_u((size_t)e * ef + 9u + 2u * h2, put_members(sub[c][2u * q + (uint32_t)h2]));
                 }
             }
         }
     }
+    if (levels) *levels = two ? 2u : 1u;
+    if (sub_pairs) *sub_pairs = n_sp;
     return n_cp;
 }
 
@@ -663,6 +753,7 @@ struct PackedSet {
     uint32_t fast_sqrt = 0;
     std::vector<float> clusters;  // cluster_table
     uint32_t n_cpairs = 0, cl_words = 0;
+    uint32_t cl_levels = 0, cl_sub_pairs = 0;  // two-level tables (cl_words >= 2)
 };
 
 static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env = -1) {
@@ -710,7 +801,7 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
     // (rt_kernel.hip kPfRel, kClRel): the cluster table is built for that rule, and
     // row 3 then holds r^2 (-inf: never hit).
     p.relative = pf_rel_env == 1 || (pf_rel_env < 0 && !p.prefilter_pays);
-    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words, p.relative);
+    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words, p.relative, &p.cl_levels, &p.cl_sub_pairs);
     if (p.relative)
         for (uint32_t sl = 0; sl < 4u * n; ++sl) {
             const size_t base = (size_t)(sl / 4u) * 4u * kGroupF4 + sl % 4u;
@@ -792,6 +883,17 @@ extern "C" int rt_scene_clusters(const rt_scene *scene, uint32_t enable_simd, fl
         if (capacity_f4 < nf4) return fail(RT_EINVAL, "rt_scene_clusters: capacity %u < %u", capacity_f4, nf4);
         memcpy(out, p.clusters.data(), (size_t)nf4 * 16u);
     }
+    return RT_OK;
+}
+
+extern "C" int rt_scene_cluster_layout(const rt_scene *scene, uint32_t enable_simd, uint32_t *out_levels,
+                                       uint32_t *out_sub_pairs) {
+    if (!scene || !out_levels || !out_sub_pairs) return fail(RT_EINVAL, "rt_scene_cluster_layout: NULL argument");
+    PackedSet p;
+    const int rc = pack_set(scene, enable_simd ? 0 : 1, p);
+    if (rc) return rc;
+    *out_levels = p.n_cpairs ? p.cl_levels : 0u;
+    *out_sub_pairs = p.cl_sub_pairs;
     return RT_OK;
 }
 

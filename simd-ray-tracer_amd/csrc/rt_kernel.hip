@@ -694,49 +694,83 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
     }
 }
 
+// One cluster-pair entry (both levels of the table share the row layout):
+// the wave's lanes that may reach cluster 0 / 1 (near the line, not wholly
+// behind the origin, and for per-lane tables inside the height slab).
+template <bool REL>
+__device__ __forceinline__ void cluster_pair(cv4f_t *e, const RayPk &ray, float oy, float dy, float slab_e0,
+                                             uint64_t &m0, uint64_t &m1) {
+    const v4f_t r0 = e[0], r1 = e[1], r3 = e[3];
+    f2 T, cc;
+    const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
+    const float t0 = REL ? __builtin_fmaf(cc.x, kClRel, r1.z) : r1.z;
+    const float t1 = REL ? __builtin_fmaf(cc.y, kClRel, r1.w) : r1.w;
+    const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
+    const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
+    m0 = ballot_and(!(v.x >= t0), !(T.x < b0));
+    m1 = ballot_and(!(v.y >= t1), !(T.y < b1));
+    if constexpr (REL) {
+        // Height slab: the line's height over the t range that can reach the
+        // cluster is c +- |D.y| srho with c = O.y + D.y T; it cannot meet a
+        // member when that range clears [ymid - yhalf, ymid + yhalf] by the
+        // lane's margin E (a ground-plane scene: rays leaving the ground cross the
+        // thin layer of small spheres only near their origin).
+        const v4f_t r4 = e[4];
+        const f2 E = __builtin_elementwise_fma(cc, f2{kSlabRel, kSlabRel}, f2{slab_e0, slab_e0});
+        const f2 c = __builtin_elementwise_fma(f2{dy, dy}, T, f2{oy, oy});
+        const f2 d = c - f2{r4.x, r4.y};
+        const f2 thr = __builtin_elementwise_fma(f2{__builtin_fabsf(dy), __builtin_fabsf(dy)}, f2{r3.z, r3.w},
+                                                 f2{r4.z, r4.w} + E);
+        m0 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
+        m1 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
+    }
+}
+
 // ps (RTK_STATS): groups += member-pair entries tested, pairs += sphere pairs
-// rechecked exactly, lane_pairs += clusters entered (per wave).
+// rechecked exactly, lane_pairs += clusters entered (per wave, both levels).
+// Tables of two or more mask words (more than 32 groups) have two levels: a
+// top cluster's entry ranges index sub-cluster entries of a few spheres each,
+// whose ranges index the member entries (rt_host.cpp cluster_table); the bound
+// of a cluster covers every sphere under it, so a skipped top cluster skips
+// its sub-clusters' members too.
 template <bool SIMD, int W, bool GS, bool REL>
 __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray,
                                                  Hit &h, PfStats *ps) {
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
     constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W, REL);
+    constexpr bool kTwoLevels = W >= 2;
     // per-lane part of the height-slab margin (REL tables; rt_host.cpp cluster_table)
     const float oy = ray.y.x, dy = ray.y.y;
     const float slab_e0 = REL ? __builtin_fmaf(__builtin_fabsf(oy), 0x1p-21f, kSlabRel) : 0.0f;
-    for (uint32_t off = 0, end = a.n_cpairs * kEntryBytes; off != end; off += kEntryBytes) {
-        cv4f_t *e = cl_entry(ct, off);
-        const v4f_t r0 = e[0], r1 = e[1];
-        const v4f_t r2 = e[2], r3 = e[3];
-        f2 T, cc;
-        const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
-        const float t0 = REL ? __builtin_fmaf(cc.x, kClRel, r1.z) : r1.z;
-        const float t1 = REL ? __builtin_fmaf(cc.y, kClRel, r1.w) : r1.w;
-        const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
-        const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-        uint64_t m0 = ballot_and(!(v.x >= t0), !(T.x < b0));
-        uint64_t m1 = ballot_and(!(v.y >= t1), !(T.y < b1));
-        if constexpr (REL) {
-            // Height slab: the line's height over the t range that can reach the
-            // cluster is c +- |D.y| srho with c = O.y + D.y T; it cannot meet a
-            // member when that range clears [ymid - yhalf, ymid + yhalf] by the
-            // lane's margin E (a ground-plane scene: rays leaving the ground cross the
-            // thin layer of small spheres only near their origin).
-            const v4f_t r4 = e[4];
-            const f2 E = __builtin_elementwise_fma(cc, f2{kSlabRel, kSlabRel}, f2{slab_e0, slab_e0});
-            const f2 c = __builtin_elementwise_fma(f2{dy, dy}, T, f2{oy, oy});
-            const f2 d = c - f2{r4.x, r4.y};
-            const f2 thr = __builtin_elementwise_fma(f2{__builtin_fabsf(dy), __builtin_fabsf(dy)}, f2{r3.z, r3.w},
-                                                     f2{r4.z, r4.w} + E);
-            m0 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
-            m1 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
-        }
-        const bool in0 = m0 != 0;
-        const bool in1 = m1 != 0;
+    // the member pairs of an entered (sub-)cluster pair entry
+    auto members = [&](cv4f_t *e, bool in0, bool in1) {
+        const v4f_t r2 = e[2];
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
         if (in0) member_pairs<W, REL>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
         if (in1) member_pairs<W, REL>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);
+    };
+    // the sub-cluster pair entries [first, first + count) of an entered top cluster
+    auto subs = [&](uint32_t first, uint32_t count) {
+        for (uint32_t off = first * kEntryBytes, end = (first + count) * kEntryBytes; off != end; off += kEntryBytes) {
+            cv4f_t *e = cl_entry(ct, off);
+            uint64_t m0, m1;
+            cluster_pair<REL>(e, ray, oy, dy, slab_e0, m0, m1);
+            members(e, m0 != 0, m1 != 0);
+        }
+    };
+    for (uint32_t off = 0, end = a.n_cpairs * kEntryBytes; off != end; off += kEntryBytes) {
+        cv4f_t *e = cl_entry(ct, off);
+        uint64_t m0, m1;
+        cluster_pair<REL>(e, ray, oy, dy, slab_e0, m0, m1);
+        if constexpr (kTwoLevels) {
+            const v4f_t r2 = e[2];
+            if (ps) ps->lane_pairs += (m0 != 0 ? 1u : 0u) + (m1 != 0 ? 1u : 0u);
+            if (m0 != 0) subs(__float_as_uint(r2.x), __float_as_uint(r2.y));
+            if (m1 != 0) subs(__float_as_uint(r2.z), __float_as_uint(r2.w));
+        } else {
+            members(e, m0 != 0, m1 != 0);
+        }
     }
     cv4f_t *gp = (cv4f_t *)a.groups;
 #pragma unroll

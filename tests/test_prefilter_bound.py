@@ -219,46 +219,76 @@ def check_clusters(rt, scene, simd, seed, require_culls=False, n_rays=4000):
     relative = bool(flags & 4)  # per-lane thresholds (rt_kernel.hip kClRel / kPfRel / kBehindRel)
     centres, radius = slot_spheres(rt, scene, simd)
     live = np.isfinite(r2p)
-    # decode the table: clusters -> member spheres (by centre and r2p) and pair indices
-    members = []
+    # decode the table: clusters -> member spheres (by centre and r2p) and pair indices;
+    # two-level tables: top entries -> sub-cluster entries -> member entries
+    levels, n_sub = rt.scene_cluster_layout(scene, simd)
+    groups = scene.SIMDSpheres.Count if simd else (scene.ScalarSpheres.Count + 3) // 4
+    assert levels == (1 if groups <= 32 else 2), "two levels exactly for tables of two or more mask words"
+    members = []  # (qx, qy, qz, t, spheres under the cluster, b, slab), both levels
     used = set()
     beta_of = {}  # per-sphere behind threshold (member rows)
+
+    def decode_members(first, count):
+        ms = []
+        for m in range(first, first + count):
+            e = tab[m]
+            # member k's pair q: bit q & 63 in the row of mask word q >> 6 (row 2, then rows 4 ..)
+            rows = [e[2]] + [e[3 + w] for w in range(1, max(1, len(e) - 3))]
+            bits = [[int(r.view(np.uint32)[2 * k]) | (int(r.view(np.uint32)[2 * k + 1]) << 32) for r in rows]
+                    for k in range(2)]
+            pair = [0, 0]
+            for w in range(2):
+                set_words = [i for i, b in enumerate(bits[w]) if b]
+                if np.isneginf(e[1][2 + w]):
+                    assert not set_words
+                    continue
+                assert len(set_words) == 1, "one mask word per member"
+                b = bits[w][set_words[0]]
+                assert b & (b - 1) == 0, "one pair bit per member"
+                pair[w] = b.bit_length() - 1 + 64 * set_words[0]
+                x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
+                s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
+                                   (r2p == t) & live)
+                assert len(s) >= 1
+                s = [k for k in s if pair[w] == int(k) >> 1]
+                assert len(s) >= 1, "member pair index is not its sphere's pair in group order"
+                s = [k for k in s if k not in used] or s  # two spheres of one pair with equal rows
+                used.add(s[0])
+                ms.append(s[0])
+                beta_of[s[0]] = np.float32(e[3][w])
+        return ms
+
+    def cluster(q, h, ms):
+        slab = (np.float32(q[3][2 + h]), np.float32(q[4][h]), np.float32(q[4][2 + h])) if relative else None
+        return (np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]), np.float32(q[1][2 + h]), ms,
+                np.float32(q[3][h]), slab)
+
+    leaves = []
+    sub_seen = set()
     for c in range(ncp):
         q = tab[c]
         u = q[2].view(np.uint32)
         for h in range(2):
             first, count = int(u[2 * h]), int(u[2 * h + 1])
-            ms = []
-            for m in range(first, first + count):
-                e = tab[m]
-                # member k's pair q: bit q & 63 in the row of mask word q >> 6 (row 2, then rows 4 ..)
-                rows = [e[2]] + [e[3 + w] for w in range(1, max(1, len(e) - 3))]
-                bits = [[int(r.view(np.uint32)[2 * k]) | (int(r.view(np.uint32)[2 * k + 1]) << 32) for r in rows]
-                        for k in range(2)]
-                pair = [0, 0]
-                for w in range(2):
-                    set_words = [i for i, b in enumerate(bits[w]) if b]
-                    if np.isneginf(e[1][2 + w]):
-                        assert not set_words
-                        continue
-                    assert len(set_words) == 1, "one mask word per member"
-                    b = bits[w][set_words[0]]
-                    assert b & (b - 1) == 0, "one pair bit per member"
-                    pair[w] = b.bit_length() - 1 + 64 * set_words[0]
-                    x, y, z, t = e[0][w], e[0][2 + w], e[1][w], e[1][2 + w]
-                    s = np.flatnonzero((centres[:, 0] == x) & (centres[:, 1] == y) & (centres[:, 2] == z) &
-                                       (r2p == t) & live)
-                    assert len(s) >= 1
-                    s = [k for k in s if pair[w] == int(k) >> 1]
-                    assert len(s) >= 1, "member pair index is not its sphere's pair in group order"
-                    s = [k for k in s if k not in used] or s  # two spheres of one pair with equal rows
-                    used.add(s[0])
-                    ms.append(s[0])
-                    beta_of[s[0]] = np.float32(e[3][w])
-            slab = (np.float32(q[3][2 + h]), np.float32(q[4][h]), np.float32(q[4][2 + h])) if relative else None
-            members.append((np.float32(q[0][h]), np.float32(q[0][2 + h]), np.float32(q[1][h]),
-                            np.float32(q[1][2 + h]), ms, np.float32(q[3][h]), slab))
-    covered = sorted(s for m in members for s in m[4])
+            if levels == 2:
+                under = []
+                for e in range(first, first + count):
+                    assert ncp <= e < ncp + n_sub and e not in sub_seen, "sub-cluster entry outside its range"
+                    sub_seen.add(e)
+                    qs, us = tab[e], tab[e][2].view(np.uint32)
+                    for h2 in range(2):
+                        ms = decode_members(int(us[2 * h2]), int(us[2 * h2 + 1]))
+                        members.append(cluster(qs, h2, ms))
+                        leaves += ms
+                        under += ms
+                members.append(cluster(q, h, under))
+            else:
+                ms = decode_members(first, count)
+                members.append(cluster(q, h, ms))
+                leaves += ms
+    if levels == 2:
+        assert len(sub_seen) == n_sub
+    covered = sorted(leaves)
     assert covered == sorted(np.flatnonzero(live)), "every hittable sphere is in exactly one cluster"
     rng = np.random.default_rng(seed)
     o, d = rays(rng, centres[live], np.abs(radius[live]).astype(F), n_rays)
