@@ -431,7 +431,8 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // RTWeekend K/S = 40/4, 28/3, 28/4, 24/4 -> 21.1k/21.9k/21.9k/21.7k (one level
     // at K 40: 19.6k); C5 at 512 spp K/S = 32/4, 24/3, 28/3, 24/2 -> 47.4k/48.2k/
     // 48.3k/48.3k (one level: 46.3k).
-    const bool two_levels = *words >= 2u;
+    const char *tl1 = getenv("RT_TWO_LEVEL_W1");  // A/B: one-word tables with two levels (kernel built with RTK_TWO_LEVEL_W1)
+    const bool two_levels = *words >= 2u || (tl1 && tl1[0] == '1');
     const uint32_t div = two_levels ? (relative ? 17u : 10u) : (relative ? 12u : 8u);
     uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / div));
     if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob

@@ -601,6 +601,9 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
 constexpr int kClWords = 4;  // pair-mask words (n_groups <= 128)
+#ifndef RTK_TWO_LEVEL_W1  // 1: one-word cluster tables walk two levels too (A/B; the host needs RT_TWO_LEVEL_W1=1)
+#define RTK_TWO_LEVEL_W1 0
+#endif
 // Per-lane thresholds (pf_relative, rt_host.cpp cluster_table "relative"):
 // cluster: e_c >= RN(cc kClRel + R_c); sphere: e >= RN(cc kPfRel + r^2) (kPfRel
 // below); behind: T < RN(b - cc kBehindRel).
@@ -739,7 +742,7 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
     constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W, REL);
-    constexpr bool kTwoLevels = W >= 2;
+    constexpr bool kTwoLevels = W >= 2 || RTK_TWO_LEVEL_W1;  // (W = 1: A/B build, host RT_TWO_LEVEL_W1=1)
     // per-lane part of the height-slab margin (REL tables; rt_host.cpp cluster_table)
     const float oy = ray.y.x, dy = ray.y.y;
     const float slab_e0 = REL ? __builtin_fmaf(__builtin_fabsf(oy), 0x1p-21f, kSlabRel) : 0.0f;
