@@ -601,6 +601,9 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
 constexpr int kClWords = 4;  // pair-mask words (n_groups <= 128)
+#ifndef RTK_SUB_SLAB  // 1: sub-clusters of per-lane tables run the height-slab test too (A/B)
+#define RTK_SUB_SLAB 1
+#endif
 #ifndef RTK_TWO_LEVEL_W1  // 1: one-word cluster tables walk two levels too (A/B; the host needs RT_TWO_LEVEL_W1=1)
 #define RTK_TWO_LEVEL_W1 0
 #endif
@@ -700,7 +703,7 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
 // One cluster-pair entry (both levels of the table share the row layout):
 // the wave's lanes that may reach cluster 0 / 1 (near the line, not wholly
 // behind the origin, and for per-lane tables inside the height slab).
-template <bool REL>
+template <bool REL, bool SLAB = REL>
 __device__ __forceinline__ void cluster_pair(cv4f_t *e, const RayPk &ray, float oy, float dy, float slab_e0,
                                              uint64_t &m0, uint64_t &m1) {
     const v4f_t r0 = e[0], r1 = e[1], r3 = e[3];
@@ -712,7 +715,7 @@ __device__ __forceinline__ void cluster_pair(cv4f_t *e, const RayPk &ray, float 
     const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
     m0 = ballot_and(!(v.x >= t0), !(T.x < b0));
     m1 = ballot_and(!(v.y >= t1), !(T.y < b1));
-    if constexpr (REL) {
+    if constexpr (REL && SLAB) {
         // Height slab: the line's height over the t range that can reach the
         // cluster is c +- |D.y| srho with c = O.y + D.y T; it cannot meet a
         // member when that range clears [ymid - yhalf, ymid + yhalf] by the
@@ -758,7 +761,7 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         for (uint32_t off = first * kEntryBytes, end = (first + count) * kEntryBytes; off != end; off += kEntryBytes) {
             cv4f_t *e = cl_entry(ct, off);
             uint64_t m0, m1;
-            cluster_pair<REL>(e, ray, oy, dy, slab_e0, m0, m1);
+            cluster_pair<REL, RTK_SUB_SLAB != 0>(e, ray, oy, dy, slab_e0, m0, m1);
             members(e, m0 != 0, m1 != 0);
         }
     };
