@@ -24,5 +24,5 @@ if out.returncode:
     print(out.stderr[-3000:])
 for k, v in rows.items():
     g = v.get
-    print(f"{k[:48]:48s} V={g('VGPRs')} S={g('SGPRs')} Vsp={g('VGPRs Spill')} Ssp={g('SGPRs Spill')} "
+    print(f"{k[-40:]:40s} V={g('VGPRs')} S={g('SGPRs')} Vsp={g('VGPRs Spill')} Ssp={g('SGPRs Spill')} "
           f"occ={g('Occupancy [waves/SIMD]')} lds={g('LDS Size [bytes/block]')}")

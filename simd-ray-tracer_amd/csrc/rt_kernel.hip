@@ -909,6 +909,14 @@ constexpr bool kFoldBeforePrimary = RTK_FOLD_BEFORE_PRIMARY != 0;
 #define RTK_FOLD_LAZY 1
 #endif
 constexpr bool kFoldLazy = RTK_FOLD_LAZY != 0;
+// 1: a secondary round shades nothing.  Its hits wait (lane mode 3, the hit
+// parked in LDS) and are shaded by the next primary round's shading block,
+// which runs anyway for that round's own hits: about one secondary ray in five
+// hits, so a secondary round's shading block ran at ~1/5 lane utilisation.
+#ifndef RTK_DEFER_SHADE
+#define RTK_DEFER_SHADE 0
+#endif
+constexpr bool kDeferShade = RTK_DEFER_SHADE != 0;
 // primary group mask words per wave tile: the LDS-image kernels keep this
 // small (it is static LDS, and C2's blocks fill the CU's 160 KB 7 times)
 template <bool GS>
@@ -1001,11 +1009,18 @@ void trace_kernel(TraceArgs a) {
     const uint64_t st_entry = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
     //            [groups 4*n_groups float4][materials 8*n_groups float4]
-    __shared__ uint64_t s_mask[kWB][MaskWords<GS>::N];
+    // the wave tile's primary group mask: one-wave workgroups keep no LDS image,
+    // so theirs is the dynamic LDS the host sizes to the scene's words (static
+    // kMaxGroups / 64 words would cost 512 B of every workgroup's allocation)
+    __shared__ uint64_t s_mask_st[SOLO ? 1 : kWB][SOLO ? 1 : MaskWords<GS>::N];
+    uint64_t *const s_maskw = SOLO ? reinterpret_cast<uint64_t *>(smem) : s_mask_st[SOLO ? 0u : threadIdx.x >> 6];
     // ring slot s of pixel pl at s * kRingStride + pl: the sample lanes of a
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
     __shared__ float4 s_ring[P > 1 ? kWB * kRing * kRingStride : 1];
+    // a hit found by a secondary round waits here (mode 3) for the next primary
+    // round's shading block: {tmin, sphere index | inside << 31}, lane-private
+    __shared__ float2 s_hit[kDeferShade ? kWB * 64u : 1u];
     const uint32_t lut_f4 = a.lut_in_lds ? 512u : 0u;  // see rtk_lds_bytes
     const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, a.lut_in_lds != 0u};
     float2 *fold = reinterpret_cast<float2 *>(smem + lut_f4);
@@ -1078,10 +1093,11 @@ void trace_kernel(TraceArgs a) {
     // every lane of a pixel keeps the fold cursor (whole-batch frontier fold)
     constexpr bool kCursorPerLane = RTK_FOLD_FRONTIER && RTK_FOLD_WHOLE && P > 1;
     float4 *ring = s_ring + sw * kRing * kRingStride + pl;
+    float2 *hit_slot = s_hit + (kDeferShade ? sw * 64u + lane : 0u);
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     // the wave tile's primary group mask, from the cull pass (rtk_launch_cull)
-    if (CULL && lane < n_words) s_mask[sw][lane] = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
+    if (CULL && lane < n_words) s_maskw[lane] = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
     const uint64_t st_c1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
@@ -1100,7 +1116,8 @@ void trace_kernel(TraceArgs a) {
 
     // owner lanes of in-image pixels (they fold until every frame is folded)
     const uint64_t folding = ballot_and(owner, valid);
-    // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left
+    // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left,
+    // 3 = a secondary round's hit waits to be shaded (kDeferShade)
     uint32_t k = j;            // this lane's next (or current) sample
     uint32_t folded = 0;       // owner: samples folded so far
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
@@ -1126,7 +1143,7 @@ void trace_kernel(TraceArgs a) {
     // = RN(Prev*((n-1)/n)) -- folded here without generating the rays.
     bool empty_tile = CULL && !a.use_sky && a.max_bounce != 0;
     if (CULL)
-        for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_mask[sw][w] == 0;
+        for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_maskw[w] == 0;
     if (empty_tile) {
         // (an all-zero running mean stays exactly zero: nothing to fold)
         if (valid && folder && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
@@ -1326,14 +1343,16 @@ void trace_kernel(TraceArgs a) {
         bool can_start = mode == 0u && ring_ok;
         uint64_t pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         const uint64_t sec = __builtin_amdgcn_ballot_w64(mode == 1u);
+        // hits parked by a secondary round, shaded by the next non-secondary round
+        const uint64_t shd = kDeferShade ? __builtin_amdgcn_ballot_w64(mode == 3u) : 0ull;
         const uint64_t alive = __builtin_amdgcn_ballot_w64(mode != 2u) | (folding & __builtin_amdgcn_ballot_w64(folded < a.frames));
         if (alive == 0) break;
         const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
         // Secondary segments run the full sphere loop; let them gather until
         // enough lanes share one (or no primary work is ready).
-        const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        const bool do_sec = sec != 0 && ((pri | shd) == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
         // (lazy: only when some lane waits for ring space, or nothing else is left)
-        const bool fold_now = !do_sec && (!kFoldLazy || (pri | sec) == 0 ||
+        const bool fold_now = !do_sec && (!kFoldLazy || (pri | sec | shd) == 0 ||
                                           (__builtin_amdgcn_ballot_w64(mode == 0u) & ~pri) != 0);
         if (kFoldBeforePrimary && fold_now) {
             // the owners fold only before a primary round (or when nothing is left to
@@ -1344,7 +1363,7 @@ void trace_kernel(TraceArgs a) {
             can_start = mode == 0u && ring_ok;
             pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         }
-        if ((pri | sec) != 0) {
+        if ((pri | sec | shd) != 0) {
             if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 if (do_sec && __builtin_popcountll(sec) < 16) { st_sparse_it += 1; st_sparse_lanes += __builtin_popcountll(sec); }
@@ -1366,24 +1385,29 @@ void trace_kernel(TraceArgs a) {
             }
             // do_sec ? mode == 1 : can_start, as one compare against a uniform mode
             // and a uniform override of the ring test (no lane-mask select)
-            const bool traces = mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
+            // (a parked lane's segment was counted by the round that traced it)
+            const bool parked = kDeferShade && !do_sec && mode == 3u;
+            const bool traces = kDeferShade ? (do_sec ? mode == 1u : (mode == 0u && ring_ok) || mode == 3u)
+                                            : mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
             if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
             if (traces) {
-                if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
-                bool done;
+                if (!do_sec && !parked) start_sample(kernel_args(), x, y, a.prev_count + k, p);
+                bool done, defer = false;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
                 } else {
                     Hit h;
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
-                    if (CULL && !do_sec) {
+                    if (parked) {
+                        // nothing to trace: the hit comes from the LDS slot below
+                    } else if (CULL && !do_sec) {
                         for (uint32_t w = 0; w < n_words; ++w) {
                             // (readfirstlane returns int: widen each half as u32, or
                             // bit 31 would sign-extend into groups 32..63)
-                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mask[sw][w]);
+                            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_maskw[w]);
                             const uint32_t hi =
-                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mask[sw][w] >> 32));
+                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_maskw[w] >> 32));
                             uint64_t m = (uint64_t)lo | ((uint64_t)hi << 32);
                             if (kStats && a.stats) st_groups += __builtin_popcountll(m);
                             while (m) {
@@ -1457,7 +1481,17 @@ void trace_kernel(TraceArgs a) {
                         sidx = h.g0;
                         inside = h.ins != 0;
                     }
-                    if (tmin == kFMax) {
+                    if (parked) {
+                        const float2 hs = *hit_slot;
+                        tmin = hs.x;
+                        sidx = __float_as_uint(hs.y) & 0x7FFFFFFFu;
+                        inside = (__float_as_uint(hs.y) >> 31) != 0u;
+                    }
+                    if (kDeferShade && do_sec && tmin != kFMax) {
+                        *hit_slot = make_float2(tmin, __uint_as_float(sidx | (inside ? 0x80000000u : 0u)));
+                        defer = true;
+                        done = false;
+                    } else if (tmin == kFMax) {
                         if (a.use_sky) {  // main.cpp:434-438
                             const float s = (p.ry.y + 1.0f) * 0.5f;
                             const float w = (1.0f - s) * 1.0f;
@@ -1493,13 +1527,13 @@ void trace_kernel(TraceArgs a) {
                     k += P;
                     mode = k < a.frames ? 0u : 2u;
                 } else {
-                    mode = 1u;
+                    mode = defer ? 3u : 1u;
                 }
             }
         }
         const uint64_t st_t1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats && a.stats && (pri | sec) != 0) {
-            const bool was_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        if (kStats && a.stats && (pri | sec | shd) != 0) {
+            const bool was_sec = sec != 0 && ((pri | shd) == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
             (was_sec ? st_cyc_sec : st_cyc_pri) += st_t1 - st_t0;
         }
         if (!kFoldBeforePrimary) fold_ring();
@@ -1905,9 +1939,11 @@ template <int P>
 static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks, hipStream_t stream) {
     const dim3 block(256), grid(n_blocks);
     const size_t lds = rtk_lds_bytes(a);
+    const size_t solo_lds = 8u * ((a->n_groups + 63u) / 64u);  // one-wave kernels: the cull mask words
 #define RTK_LAUNCH(S, R, C, G) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P, G>), grid, block, lds, stream, *a)
 #define RTK_LAUNCH_SOLO(S, C, K) \
-    hipLaunchKernelGGL((rtk::trace_kernel<S, kSrcSmem, C, P, true, true, K>), dim3(4u * n_blocks), dim3(64), 0, stream, *a)
+    hipLaunchKernelGGL((rtk::trace_kernel<S, kSrcSmem, C, P, true, true, K>), dim3(4u * n_blocks), dim3(64), solo_lds, \
+                       stream, *a)
     if (a->solo) {  // one wave per workgroup, no LDS image (the host clears the *_in_lds flags)
         // one walk per kernel for the culled production shapes; others dispatch at run time
         if constexpr (P == 4 || P == 8 || P == 16) {
