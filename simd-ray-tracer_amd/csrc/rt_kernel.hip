@@ -988,6 +988,16 @@ struct Shape {
 // pressure of the others out of the trace loop (C2 +4 % with only the W = 1
 // walk compiled in).  The exact all-groups loop stays in every variant (rounds
 // whose directions leave the prefilter's |D|^2 bound).
+// Occupancy target of the one-wave kernels per secondary walk: the two-word
+// scene-wide cluster walk (C5: 256 spheres) takes 8 waves/SIMD (63 VGPRs, the
+// cull mask in dynamic LDS leaves room for 32 workgroups per CU): C5 +2.7 %
+// same-box, while C2 (one word) and RTWeekend (four per-lane words) lose
+// 1.5 % and 0.5 % at 8 and keep 7.
+#ifndef RTK_SOLO_WAVES_CL2
+#define RTK_SOLO_WAVES_CL2 8
+#endif
+constexpr int solo_waves(int walk) { return walk == kWalkCl2 ? RTK_SOLO_WAVES_CL2 : RTK_SOLO_WAVES_PER_SIMD; }
+
 template <int WALK> struct Walk {
     static constexpr int W = WALK == kWalkCl2 || WALK == kWalkCl2Rel ? 2 : WALK == kWalkCl4 || WALK == kWalkCl4Rel ? 4 : 1;
     static constexpr bool REL = WALK == kWalkCl1Rel || WALK == kWalkCl2Rel || WALK == kWalkCl4Rel;
@@ -995,7 +1005,7 @@ template <int WALK> struct Walk {
 };
 
 template <bool SIMD, int SRC, bool CULL, int P, bool GS, bool SOLO = false, int WALK = kWalkAny>
-__global__ __launch_bounds__(SOLO ? 64 : 256, SOLO ? RTK_SOLO_WAVES_PER_SIMD : SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1)
+__global__ __launch_bounds__(SOLO ? 64 : 256, SOLO ? solo_waves(WALK) : SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1)
 void trace_kernel(TraceArgs a) {
     static_assert(!GS || SRC == kSrcSmem, "a scene in HBM is read through the scalar cache");
     static_assert(!SOLO || GS, "a one-wave workgroup keeps no LDS image");
