@@ -601,8 +601,11 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
 constexpr int kClWords = 4;  // pair-mask words (n_groups <= 128)
-#ifndef RTK_MEMBER_BEHIND  // 1: member pairs also take the behind-origin test (A/B)
+#ifndef RTK_MEMBER_BEHIND  // 1: member pairs of scene-wide tables also take the behind-origin test (A/B)
 #define RTK_MEMBER_BEHIND 1
+#endif
+#ifndef RTK_MEMBER_BEHIND_REL  // the same for per-lane (REL) tables (A/B)
+#define RTK_MEMBER_BEHIND_REL 0
 #endif
 #ifndef RTK_SUB_SLAB  // 1: sub-clusters of per-lane tables run the height-slab test too (A/B)
 #define RTK_SUB_SLAB 1
@@ -685,12 +688,13 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         const float t1 = REL ? __builtin_fmaf(cc.y, kPfRel, r1.w) : r1.w;
         const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-        // (RTK_MEMBER_BEHIND=0, A/B: members take the near-line test only; the behind rule
-        // stays at the cluster level.  Either way a skipped pair is a proven miss.)
-        const uint64_t f0m = RTK_MEMBER_BEHIND ? ballot_and(!(v.x >= t0), !(T.x < b0))
-                                               : __builtin_amdgcn_ballot_w64(!(v.x >= t0));
-        const uint64_t f1m = RTK_MEMBER_BEHIND ? ballot_and(!(v.y >= t1), !(T.y < b1))
-                                               : __builtin_amdgcn_ballot_w64(!(v.y >= t1));
+        // Members of per-lane (REL) tables take the near-line test only: their behind
+        // threshold is a per-lane FMA, and the rule stays at the cluster level
+        // (RTWeekend +2.7 % same box; C2's scene-wide table loses 1.7 % without it).
+        // Either way a skipped pair is a proven miss.
+        constexpr bool kBehind = REL ? RTK_MEMBER_BEHIND_REL != 0 : RTK_MEMBER_BEHIND != 0;
+        const uint64_t f0m = kBehind ? ballot_and(!(v.x >= t0), !(T.x < b0)) : __builtin_amdgcn_ballot_w64(!(v.x >= t0));
+        const uint64_t f1m = kBehind ? ballot_and(!(v.y >= t1), !(T.y < b1)) : __builtin_amdgcn_ballot_w64(!(v.y >= t1));
         const bool f0 = f0m != 0, f1 = f1m != 0;
         uint64_t bw0[W], bw1[W];  // member 0 and 1 bits in word w
 #pragma unroll
