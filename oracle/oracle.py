@@ -60,6 +60,11 @@ def lib() -> ctypes.CDLL:
         L.or_encode_rgba8.argtypes = [c_void_p, c_void_p, c_uint64, c_int]
         L.or_srgb_channel.restype = c_float
         L.or_srgb_channel.argtypes = [c_float, c_int]
+        L.or_reflectance.restype = c_float
+        L.or_reflectance.argtypes = [c_float, c_float]
+        L.or_blend_store.argtypes = [c_uint32, c_void_p, c_void_p, c_void_p]
+        L.or_emit_attenuate.argtypes = [c_void_p] * 4
+        L.or_srgb_n.argtypes = [c_void_p, c_void_p, c_uint64]
         _L = L
         set_lut(np.fromfile(LUT_PATH, dtype=np.float32))
     return _L

@@ -403,11 +403,16 @@ static void primary_ray(const trace_ctx *c, uint32_t x, uint32_t y, uint64_t *rn
 
 /* main.cpp:446-481: emission/attenuation and the bounce direction.
  * hit_n is the un-normalised HitNormal, new_o the next origin. */
+static void emit_attenuate(const float emis[3], const float color[3], float att[3], float out[3])
+{
+    for (int k = 0; k < 3; ++k) out[k] = out[k] + emis[k] * att[k];   /* main.cpp:446 */
+    for (int k = 0; k < 3; ++k) att[k] = att[k] * color[k];           /* main.cpp:447 */
+}
+
 static void shade(const or_material *m, const float hit_n[3], int inside, uint64_t *rng,
                   float dir[3], float att[3], float out[3])
 {
-    for (int k = 0; k < 3; ++k) out[k] = out[k] + (&m->emissive.x)[k] * att[k];
-    for (int k = 0; k < 3; ++k) att[k] = att[k] * (&m->color.x)[k];
+    emit_attenuate(&m->emissive.x, &m->color.x, att, out);
     float n[3];
     or_normalize(hit_n, n);
     float k2 = 2.0f * dot3(dir, n);
@@ -794,4 +799,20 @@ uint64_t or_fnv1a64(const void *data, uint64_t nbytes)
     uint64_t h = 0xcbf29ce484222325ULL;
     for (uint64_t i = 0; i < nbytes; ++i) { h ^= p[i]; h *= 0x100000001b3ULL; }
     return h;
+}
+
+/* Exported pieces of the colour path, for differential tests against the
+ * reference's own compiled main.cpp lines (oracle/_ref/librefmath.so). */
+float or_reflectance(float cos_theta, float eta) { return reflectance(cos_theta, eta); }
+void or_blend_store(uint32_t prev_count, const float out3[3], float prev4[4], uint32_t *px)
+{
+    blend_store(prev_count, out3, prev4, px);
+}
+void or_emit_attenuate(const float emis[3], const float color[3], float att[3], float out[3])
+{
+    emit_attenuate(emis, color, att, out);
+}
+void or_srgb_n(const float *in, float *out, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; ++i) out[i] = srgb(in[i]);
 }

@@ -11,14 +11,16 @@
  *   - camera basis      main.cpp:776-838 (x87 fcos/fsin, x64_math.h:728-746)
  *   - PCG / RandomFloat base.h:951-997, per-thread seed mixer main.cpp:667-678
  *
- * Parity pin: the reference's math layer (base.h + x64_math.h)
- * is compiled from where it lies into oracle/_ref/librefmath.so (Makefile)
- * and checked against these primitives; the known-answer values and the
- * end-to-end bounce-segment counts recorded from the verbatim reference in
- * SURVEY.md §7/§8(c) are reproduced (tests/test_oracle_reference.py).  The
- * survey's FNV-1a image hashes are NOT reproduced (their hashing protocol is
- * not recoverable).  main.cpp itself needs
- * <emscripten/atomic.h>, absent here, so the full reference is unbuildable.
+ * Parity pin: the reference's own code -- base.h + x64_math.h
+ * and main.cpp lines 7-640 (scene generators, Reflectance, LinearToSRGB,
+ * ColorFromV4, RenderTile, RenderTileScalar) -- is compiled from where it
+ * lies into oracle/_ref/librefmath.so (Makefile, ref_harness.cpp) and checked
+ * against this restatement: primitives, the colour path, the built-in scenes
+ * and whole framebuffers (tests/test_oracle_reference.py,
+ * tests/test_oracle_vs_reference_render.py).  Known-answer values and the
+ * end-to-end bounce-segment counts recorded in SURVEY.md §7/§8(c) are
+ * reproduced too.  The survey's FNV-1a image hashes are not (their hashing
+ * protocol is not recoverable).
  */
 #ifndef RT_ORACLE_H
 #define RT_ORACLE_H
@@ -104,6 +106,10 @@ float or_srgb_channel(float l, int pow_mode);
 void  or_group_test(const float o[3], const float d[3], const or_group *g, float dist_out[4], float t_out[4]);
 float or_horizontal_min(const float v[4], uint32_t *lane);
 void  or_cross(const float a[3], const float b[3], float out[3]);
+float or_reflectance(float cos_theta, float eta);                                 /* main.cpp:292-300 */
+void  or_blend_store(uint32_t prev_count, const float out3[3], float prev4[4], uint32_t *px); /* :484-492 */
+void  or_emit_attenuate(const float emis[3], const float color[3], float att[3], float out[3]); /* :446-447 */
+void  or_srgb_n(const float *in, float *out, uint64_t n);                        /* :312-329, n values */
 
 #ifdef __cplusplus
 }

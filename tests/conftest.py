@@ -114,19 +114,27 @@ def orc():
 
 @pytest.fixture(scope="session")
 def refmath():
-    """The reference's own math layer (base.h + x64_math.h compiled from
-    /root/reference by oracle/Makefile); only present in the build container."""
+    """The reference's own code (base.h + x64_math.h and main.cpp:7-640,
+    compiled from /root/reference by `make -C oracle ref`); only present in the
+    build container."""
     import ctypes
     path = ROOT / "oracle" / "_ref" / "librefmath.so"
     if not path.exists():
         pytest.skip("oracle/_ref/librefmath.so not built (needs /root/reference)")
     L = ctypes.CDLL(str(path))
-    f, v, u32, u64p = ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p
+    f, v, u32, u64p, u64 = ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64
     for name, res, args in [("ref_pcg", u32, [u64p]), ("ref_random_float", f, [u64p, f, f]), ("ref_rsqrt", f, [f]),
                             ("ref_sqrt", f, [f]), ("ref_min", f, [f, f]), ("ref_normalize", None, [v, v]),
                             ("ref_normalize_fast", None, [v, v]), ("ref_cross", None, [v, v, v]),
                             ("ref_dot", f, [v, v]), ("ref_cos", f, [f]), ("ref_sin", f, [f]),
-                            ("ref_horizontal_min", f, [v]), ("ref_group_test", None, [v, v, v, v, v, v, v, v])]:
+                            ("ref_horizontal_min", f, [v]), ("ref_group_test", None, [v, v, v, v, v, v, v, v]),
+                            ("ref_reflectance", f, [f, f]), ("ref_linear_to_srgb", f, [f]),
+                            ("ref_color_from_v4", u32, [v]), ("ref_encode_rgba8", None, [v, v, u64]),
+                            ("ref_linear_to_srgb_n", None, [v, v, u64]), ("ref_blend_store", None, [u32, v, v, v]),
+                            ("ref_emit_attenuate", None, [v, v, v, v]),
+                            ("ref_scene_builtin", ctypes.c_int, [ctypes.c_int, v, u32, v, u32, v, u32, v]),
+                            ("ref_render", None, [v, u32, v, u32, v, u32, u32, v, u32, u32, u32, u32, ctypes.c_int,
+                                                  v, v, v, v])]:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
