@@ -91,6 +91,9 @@ def parse():
                    help="single-process multi-GPU gather: RCCL, peer copies, or RCCL where it can be used")
     p.add_argument("--no-verify", action="store_true", help="multi-GPU: skip the whole-frame check (on by default)")
     p.add_argument("--frames", type=int, default=256, help="onrender: completed frames per measured run")
+    p.add_argument("--modes", default="static,moving", help="onrender: camera modes to run (static, moving)")
+    p.add_argument("--no-register", action="store_true",
+                   help="onrender: hand frames out through the library's staging buffer (no registered image)")
     a = p.parse_args()
     if a.config == "onrender":
         return a
@@ -357,6 +360,9 @@ def main_multi_device(args):
         else rt.RT_MULTI_AUTO
     multi = rt.Multi(devices, transport=transport)
     multi.upload_scene(scene)
+    # every buffer a call of this geometry needs, allocated now: no call of the
+    # timed region allocates or waits for a device (rt_multi_reserve)
+    multi.reserve(W, H, args.band_rows)
     full = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     ctr = torch.zeros(args.warmup + args.steps + 2, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream()
@@ -398,6 +404,7 @@ def main_multi_device(args):
     if any(n != rays_per_step for n in timed):
         raise SystemExit(f"bench.py: timed steps counted {timed} segments, expected {rays_per_step} each")
     per_dev_ms = multi.last_trace_ms(len(devices))
+    gather_ms = multi.last_gather_ms()
     minfo = multi.info()
     call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     frame = full.clone()
@@ -405,7 +412,6 @@ def main_multi_device(args):
     dev = rt.Device(d0)
     dev.upload_scene(scene)
     ref, one_ms, one_rays = one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, min(args.steps, 5))
-    one_info = dev.last_info()
     verified = bool(torch.equal(frame, ref)) and one_rays == rays_per_step
     workload = workload_name(args, W, H, S, N, B)
     gather = ("RCCL grouped send/recv to devices[0] (ncclCommInitAll) + rt_assemble scatter, overlapping the next "
@@ -422,6 +428,10 @@ def main_multi_device(args):
     line["cold"] = {"ms": round(cold_ms, 3), "note": "first call for this camera/geometry on every device (cull "
                     "passes + untrained tile orders + RCCL/peer setup), wall clock incl. its synchronisation"}
     line["per_device_trace_ms"] = [round(v, 3) for v in per_dev_ms]
+    line["gather_ms"] = round(gather_ms, 4)
+    line["gather"] = {"ms": round(gather_ms, 4), "bytes": W * H * 4,
+                      "note": "last timed call: from every device's trace done to the frame assembled on devices[0] "
+                              "(HIP events on its gather stream: band transfer + scatter, rt_multi_last_gather_ms)"}
     line["call_ms_events"] = round(call_ms, 3)
     line["one_gpu"] = {"ms_per_frame": round(one_ms, 3), "device": d0,
                        "speedup_vs_one_gpu": round(one_ms / (elapsed / args.steps * 1e3), 3),
@@ -430,8 +440,7 @@ def main_multi_device(args):
     # the roofline of the slowest device's share (its trace kernel; counters: the committed share record)
     slowest = max(range(len(devices)), key=lambda i: per_dev_ms[i])
     rows0 = rt.band_local_rows(H, band_rows, args.gpus, slowest)
-    share_info = {"LanesPerPixel": 16 if rows0 * W < 256 * 1536 else 8 if rows0 * W < 256 * 6144 else 4,
-                  "OneWaveGroups": one_info["OneWaveGroups"], "Walk": one_info["Walk"]}
+    share_info = multi.shard_info(slowest)  # what the slowest device's last launch really ran
     line["roofline"] = roofline(args, share_info, per_dev_ms[slowest], rays_per_step // args.gpus, rows0, W, N,
                                 workload, args.gpus)
     line["roofline"]["device"] = slowest
@@ -478,8 +487,12 @@ def main_onrender(args):
     for devs in device_sets:
         for (W, H) in sizes:
             for mode, keys in (("static", 0), ("moving", rt.KEY_LEFT)):
+                if mode not in args.modes.split(","):
+                    continue
                 rt.on_init(devs if len(devs) > 1 else None)
                 img = np.zeros((H, W), np.uint32)
+                if not args.no_register:  # the platform's persistent image (wasm/wasm.cpp:179)
+                    rt.on_render_register_image(img)
                 warm = 0
                 while warm < 8:  # code objects, allocations, the first cull pass
                     ok, _, _ = rt.on_render(img, scene, True, keys)
@@ -495,7 +508,8 @@ def main_onrender(args):
                         done += 1
                         rays += r
                 wall = time.perf_counter() - t0
-                run = {"devices": devs, "width": W, "height": H, "mode": mode, "frames": done, "calls": calls,
+                run = {"devices": devs, "width": W, "height": H, "mode": mode,
+                       "image": "staged" if args.no_register else "registered", "frames": done, "calls": calls,
                        "rays": rays, "mrays_per_s": round(rays / wall / 1e6, 1),
                        "ms_per_frame": round(wall / done * 1e3, 4)}
                 if has_profile:
@@ -560,6 +574,7 @@ def main():
     rows = [rt.band_local_rows(H, band_rows, bands, r) for r in range(bands)]
     maxr = max(rows)
     band_index = args.sim_index if bands != world else rank
+    dev.reserve(W, maxr)  # launch buffers for this band geometry: no timed launch allocates (rt_device_reserve)
     # Two frame slots: frame i's band image is gathered to rank 0 while frame
     # i+1 is traced; rank 0 assembles frame i before frame i+2 reuses its slot.
     # The gather is the C-ABI's RCCL band gather (rt_comm_gather_bands: grouped

@@ -243,8 +243,21 @@ typedef struct rt_trace_info {
                                  run-time dispatch, 1 per-group loops, 2/3/4
                                  cluster walk with 1/2/4 mask words, 5/6/7
                                  the same with per-lane thresholds           */
+    uint32_t BufferGrowths;   /* launch-buffer (re)allocations on this device
+                                 so far (tile lists, cull masks): constant
+                                 across launches that rt_device_reserve covers */
 } rt_trace_info;
 int rt_trace_last_info(rt_device *dev, rt_trace_info *out);
+
+/* Pre-sizes the device's launch buffers (tile order / cost / live lists, the
+ * cull pass's masks and counters) for bands of up to `width` x `local_rows`
+ * pixels under every lanes-per-pixel shape rt_trace may pick, so that no later
+ * rt_trace of such a band allocates or waits for the device (growing a buffer
+ * otherwise synchronises the launch's stream).  Masks are sized for the
+ * current scene; rt_scene_upload re-applies the reservation for a larger one.
+ * Waits for the device.  (New; the reference's arena is sized once in OnInit,
+ * main.cpp:658.) */
+int rt_device_reserve(rt_device *dev, uint32_t width, uint32_t local_rows);
 
 /* ColorFromV4(LinearToSRGB(v)) (main.cpp:312-346, the store at :490) over a
  * device-resident running mean: n_pixels v4 f32 -> RGBA8, both DEVICE
@@ -305,8 +318,13 @@ int rt_multi_scene_upload(rt_multi *m, const rt_scene *scene);
  * enqueued on `stream` afterwards sees the gathered frame.  The traces read
  * nothing of the caller's and do not wait for that prior work: each device
  * alternates between two band-image slots, so call k's gather overlaps call
- * k+1's traces.  A continuation's PreviousRayCount must equal the frames the
- * resident means hold (RT_EINVAL otherwise); a failed call drops them. */
+ * k+1's traces.  A continuation's PreviousRayCount must equal the count the
+ * resident means were left at (RT_EINVAL otherwise): after a call with
+ * PreviousRayCount P and Frames F that is P + F -- also for a restart with
+ * RT_FLAG_ACCUM_ZERO and P > 0, whose frames were folded with the weights of
+ * P, P + 1, ... (main.cpp:484-487), as rt_trace does.  A failed call drops
+ * the resident means.  Every entry point that switches devices restores the
+ * caller's current HIP device before it returns. */
 int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
                    void *stream);
 int rt_multi_synchronize(rt_multi *m);
@@ -325,6 +343,23 @@ int rt_multi_get_info(rt_multi *m, rt_multi_info *out);
  * stream) of the last rt_multi_trace call, devices[i] -> ms_out[i]; count >=
  * the device count.  Waits for those traces to finish. */
 int rt_multi_last_trace_ms(rt_multi *m, float *ms_out, uint32_t count);
+
+/* The last call's gather time (ms, HIP events on devices[0]'s gather stream):
+ * from the moment every device's trace has finished to the frame (and mean)
+ * assembled -- the band transfer (RCCL or peer copies) plus the scatter. */
+int rt_multi_last_gather_ms(rt_multi *m, float *ms_out);
+
+/* rt_trace_last_info of devices[index] for the last call (RT_EINVAL when that
+ * device traced nothing); may wait for its cull totals. */
+int rt_multi_shard_info(rt_multi *m, uint32_t index, rt_trace_info *out);
+
+/* Pre-sizes every device's band images and launch buffers (rt_device_reserve)
+ * and devices[0]'s gather staging for frames up to width x height in
+ * band_rows-row bands (0 = 8), so no rt_multi_trace of that geometry
+ * allocates; RT_MULTI_RESERVE_MEAN also sizes the staging of the gathered
+ * running mean (cam->PreviousImage).  Waits for the devices. */
+#define RT_MULTI_RESERVE_MEAN 1u
+int rt_multi_reserve(rt_multi *m, uint32_t width, uint32_t height, uint32_t band_rows, uint32_t flags);
 
 /* ----------------------------------- several GPUs, one process per GPU (RCCL) */
 
@@ -440,17 +475,28 @@ int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
 int rt_on_render_wait(void);
 int rt_on_shutdown(void);
 
+/* Opt-in fast hand-out.  By default rt_on_render copies a completed frame
+ * into `image` through a pinned staging buffer the library owns (one DMA,
+ * then one host copy; the reference's CopyImage, main.cpp:688-697).  A caller
+ * that renders into the same host buffer every frame (the platform's image,
+ * wasm/wasm.cpp:179) may register it: the library page-locks the `bytes` at
+ * `data`, and frames for an image whose Data is `data` then arrive by one DMA
+ * straight into it.  The caller must keep the buffer allocated until
+ * rt_on_render_unregister_image or rt_on_shutdown, which unlock it.  A second
+ * registration replaces the first.  Returns RT_OK, RT_EINVAL (not initialised,
+ * NULL, 0 bytes) or RT_EIO (the driver refused to page-lock it). */
+int rt_on_render_register_image(void *data, uint64_t bytes);
+int rt_on_render_unregister_image(void);
+
 /* Where rt_on_render's time goes (cumulative since init or the last reset).
- * Each frame's RGBA8 image and ray count are copied to pinned host memory by
- * the frame's own stream work (a GPU-side DMA after the trace), so handing a
- * completed frame out is a host copy (the reference's CopyImage,
- * main.cpp:688-697) and needs no GPU round trip. */
+ * A frame is handed out by rt_on_render after the next frame is launched, so
+ * the copy runs beside that frame's trace. */
 typedef struct rt_on_render_profile {
     uint64_t Calls;          /* rt_on_render calls                                   */
     uint64_t FramesLaunched; /* frames started (trace + its copies to the host)      */
     uint64_t FramesCopied;   /* completed frames handed to the caller's image        */
     double CallMs;           /* host time inside rt_on_render                         */
-    double HostCopyMs;       /* of which: pinned frame -> caller image (CopyImage)    */
+    double HostCopyMs;       /* of which: frame -> caller image (CopyImage: DMA [+ host copy]) */
     double HostWaitMs;       /* of which: waiting for an in-flight frame (reset/move) */
     double GpuFrameMs;       /* sum of completed frames' launch -> done GPU time      */
 } rt_on_render_profile;

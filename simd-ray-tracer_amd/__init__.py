@@ -91,7 +91,7 @@ class RtTraceDesc(ctypes.Structure):
 class RtTraceInfo(ctypes.Structure):  # rt_trace_last_info
     _fields_ = [("SegmentsFolded", c_uint64)] + [(n, c_uint32) for n in (
         "LanesPerPixel", "TilesTotal", "TilesTraced", "CullPassRan", "OrderedLaunches", "ClusteredWalk",
-        "GroupsPerRuleSet", "SplitHeadFrames", "OneWaveGroups", "Walk")]
+        "GroupsPerRuleSet", "SplitHeadFrames", "OneWaveGroups", "Walk", "BufferGrowths")]
 
 
 class RtMultiInfo(ctypes.Structure):  # rt_multi_get_info
@@ -105,6 +105,7 @@ class RtOnRenderProfile(ctypes.Structure):  # rt_on_render_get_profile
 
 
 RT_MULTI_AUTO, RT_MULTI_RCCL, RT_MULTI_PEER = 0, 1, 2
+RT_MULTI_RESERVE_MEAN = 1
 RT_COMM_ID_BYTES = 128
 
 for _t, _n in ((RtV3, 16), (RtMaterial, 48), (RtScalarSphere, 80), (RtSphereGroup, 64), (RtArray, 16),
@@ -139,6 +140,10 @@ SIGNATURES = {
     "rt_multi_synchronize": (c_int, [c_void_p]),
     "rt_multi_get_info": (c_int, [c_void_p, POINTER(RtMultiInfo)]),
     "rt_multi_last_trace_ms": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "rt_multi_last_gather_ms": (c_int, [c_void_p, POINTER(c_float)]),
+    "rt_multi_shard_info": (c_int, [c_void_p, c_uint32, POINTER(RtTraceInfo)]),
+    "rt_multi_reserve": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, c_uint32]),
+    "rt_device_reserve": (c_int, [c_void_p, c_uint32, c_uint32]),
     "rt_comm_unique_id": (c_int, [c_void_p]),
     "rt_comm_create": (c_int, [c_int, c_void_p, c_uint32, c_uint32, POINTER(c_void_p)]),
     "rt_comm_destroy": (c_int, [c_void_p]),
@@ -157,6 +162,8 @@ SIGNATURES = {
     "rt_on_init_devices": (c_int, [POINTER(RtInitParams), POINTER(c_int), c_uint32]),
     "rt_on_render": (c_int, [POINTER(RtImage), RtRenderParams, c_uint32, POINTER(c_uint64), POINTER(c_double)]),
     "rt_on_render_wait": (c_int, []),
+    "rt_on_render_register_image": (c_int, [c_void_p, c_uint64]),
+    "rt_on_render_unregister_image": (c_int, []),
     "rt_on_shutdown": (c_int, []),
     "rt_on_render_get_profile": (c_int, [POINTER(RtOnRenderProfile), c_int]),
     "rt_image_write_ppm": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
@@ -362,6 +369,10 @@ class Device:
         _check(lib().rt_trace_last_info(self.handle, ctypes.byref(info)), "rt_trace_last_info")
         return {n: int(getattr(info, n)) for n, _ in RtTraceInfo._fields_}
 
+    def reserve(self, width: int, local_rows: int) -> None:
+        """rt_device_reserve: pre-size the launch buffers for bands up to width x local_rows."""
+        _check(lib().rt_device_reserve(self.handle, width, local_rows), "rt_device_reserve")
+
     def debug_stats(self, reset: bool = True):
         """RT_STATS=1 scheduling counters (see rt_debug_stats), or None when disabled."""
         out = np.zeros(32, np.uint64)
@@ -439,6 +450,23 @@ class Multi:
         out = (c_float * n_devices)()
         _check(lib().rt_multi_last_trace_ms(self.handle, out, n_devices), "rt_multi_last_trace_ms")
         return [float(v) for v in out]
+
+    def last_gather_ms(self) -> float:
+        """The last call's gather (transfer + scatter) time on devices[0] (waits for it)."""
+        ms = c_float(0.0)
+        _check(lib().rt_multi_last_gather_ms(self.handle, ctypes.byref(ms)), "rt_multi_last_gather_ms")
+        return float(ms.value)
+
+    def shard_info(self, index: int) -> dict:
+        """rt_trace_last_info of devices[index] for the last call."""
+        info = RtTraceInfo()
+        _check(lib().rt_multi_shard_info(self.handle, index, ctypes.byref(info)), "rt_multi_shard_info")
+        return {n: int(getattr(info, n)) for n, _ in RtTraceInfo._fields_}
+
+    def reserve(self, width: int, height: int, band_rows: int = 8, mean: bool = False) -> None:
+        """rt_multi_reserve: pre-size every buffer a call of this geometry needs."""
+        _check(lib().rt_multi_reserve(self.handle, width, height, band_rows, RT_MULTI_RESERVE_MEAN if mean else 0),
+               "rt_multi_reserve")
 
     def info(self) -> dict:
         i = RtMultiInfo()
@@ -531,6 +559,18 @@ def on_render(image: np.ndarray, scene_index: int, enable_simd: bool = True, key
                             ctypes.byref(rays), ctypes.byref(ms))
     _check(rc, "rt_on_render")
     return bool(rc), int(rays.value), float(ms.value)
+
+
+def on_render_register_image(image: np.ndarray) -> None:
+    """rt_on_render_register_image: page-lock `image` so frames handed to it
+    arrive by one DMA; keep it alive until on_render_unregister_image()."""
+    assert image.dtype == np.uint32 and image.flags.c_contiguous
+    _check(lib().rt_on_render_register_image(c_void_p(image.ctypes.data), c_uint64(image.nbytes)),
+           "rt_on_render_register_image")
+
+
+def on_render_unregister_image() -> None:
+    _check(lib().rt_on_render_unregister_image(), "rt_on_render_unregister_image")
 
 
 def on_render_wait() -> None:

@@ -16,6 +16,7 @@
 #include <string.h>
 #include <time.h>
 
+#include "rt_kernel.h"
 #include "rt_trace.h"
 
 #include "rsqrt_table_intel.inc"
@@ -84,10 +85,14 @@ struct App {
     hipStream_t stream = nullptr;  // traces
     hipStream_t copy = nullptr;    // the hand-out DMA, beside the next frame's trace
     bool in_flight = false;
-    // The caller's image is page-locked (hipHostRegister) once the same buffer
-    // comes back a second time, so the hand-out is one DMA straight into it.
-    void *seen_ptr = nullptr, *reg_ptr = nullptr;
-    size_t seen_bytes = 0, reg_bytes = 0;
+    // A caller image registered with rt_on_render_register_image is page-locked,
+    // so the hand-out is one DMA straight into it.  Any other image gets the
+    // frame through a pinned staging buffer the library owns (DMA, then one host
+    // copy): the library never page-locks memory it was not handed explicitly.
+    void *reg_ptr = nullptr;
+    size_t reg_bytes = 0;
+    void *staging = nullptr;
+    size_t staging_bytes = 0;
     rt_camera_info cam;
     rt_on_render_profile prof;
 };
@@ -122,27 +127,26 @@ void unregister_image() {
 }
 
 // The completed frame in d_cur[slot] into the caller's image (CopyImage,
-// main.cpp:688-697): one DMA on the copy stream, into the page-locked image
-// when the caller keeps passing the same buffer (else HIP stages it).
+// main.cpp:688-697): one DMA on the copy stream, straight into a registered
+// image, else into the library's pinned staging buffer and from there by a
+// host copy.
 int hand_out(const rt_image *image, uint32_t slot) {
     if (!image->Data) return RT_OK;
     const size_t bytes = (size_t)g_app.width * g_app.height * 4u;
     const double t = now_ms();
-    if (image->Data == g_app.seen_ptr && bytes == g_app.seen_bytes &&
-        (image->Data != g_app.reg_ptr || bytes != g_app.reg_bytes)) {
-        unregister_image();
-        if (hipHostRegister(image->Data, bytes, hipHostRegisterDefault) == hipSuccess) {
-            g_app.reg_ptr = image->Data;
-            g_app.reg_bytes = bytes;
-        } else {
-            (void)hipGetLastError();  // stays pageable: the staged copy below still works
-        }
+    const bool direct = image->Data == g_app.reg_ptr && bytes <= g_app.reg_bytes;
+    if (!direct && bytes > g_app.staging_bytes) {
+        if (g_app.staging) (void)hipHostFree(g_app.staging);
+        g_app.staging = nullptr;
+        g_app.staging_bytes = 0;
+        if (hipHostMalloc(&g_app.staging, bytes, hipHostMallocDefault) != hipSuccess) return RT_ENOMEM;
+        g_app.staging_bytes = bytes;
     }
-    g_app.seen_ptr = image->Data;
-    g_app.seen_bytes = bytes;
-    if (hipMemcpyAsync(image->Data, g_app.d_cur[slot], bytes, hipMemcpyDeviceToHost, g_app.copy) != hipSuccess ||
+    void *dst = direct ? image->Data : g_app.staging;
+    if (hipMemcpyAsync(dst, g_app.d_cur[slot], bytes, hipMemcpyDeviceToHost, g_app.copy) != hipSuccess ||
         hipStreamSynchronize(g_app.copy) != hipSuccess)
         return RT_EIO;
+    if (!direct) memcpy(image->Data, g_app.staging, bytes);
     g_app.prof.HostCopyMs += now_ms() - t;
     g_app.prof.FramesCopied += 1;
     return RT_OK;
@@ -156,6 +160,7 @@ extern "C" int rt_on_init(rt_init_params *params) {
 }
 
 extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices, uint32_t count) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!hip_devices || count == 0) return RT_EINVAL;
     if (params) {  // main.cpp:646-650
         static const char kTitle[] = "SIMD Ray Tracer";
@@ -198,6 +203,7 @@ static int on_render(const rt_image *image, rt_render_params params, uint32_t ke
 
 extern "C" int rt_on_render(const rt_image *image, rt_render_params params, uint32_t keys,
                             uint64_t *out_total_rays_cast, double *out_time_elapsed_ms) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     const double t = now_ms();
     const int rc = on_render(image, params, keys, out_total_rays_cast, out_time_elapsed_ms);
     g_app.prof.Calls += 1;
@@ -337,10 +343,37 @@ extern "C" int rt_on_render_get_profile(rt_on_render_profile *out, int reset) {
 
 extern "C" int rt_on_render_wait(void) { return g_app.ready ? wait_frame() : RT_OK; }
 
+extern "C" int rt_on_render_register_image(void *data, uint64_t bytes) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    if (!g_app.ready || !data || bytes == 0) return RT_EINVAL;
+    if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
+    if (data == g_app.reg_ptr && bytes == g_app.reg_bytes) return RT_OK;
+    // the copy stream may still be writing into the old registration only
+    // inside a hand-out, which is synchronous, so it is idle here
+    unregister_image();
+    if (hipHostRegister(data, (size_t)bytes, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return RT_EIO;
+    }
+    g_app.reg_ptr = data;
+    g_app.reg_bytes = (size_t)bytes;
+    return RT_OK;
+}
+
+extern "C" int rt_on_render_unregister_image(void) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    if (!g_app.ready) return RT_OK;
+    if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
+    unregister_image();
+    return RT_OK;
+}
+
 extern "C" int rt_on_shutdown(void) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!g_app.ready) return RT_OK;
     wait_frame();
     unregister_image();
+    if (g_app.staging) (void)hipHostFree(g_app.staging);
     (void)hipFree(g_app.d_prev);
     (void)hipFree(g_app.d_cur[0]);
     (void)hipFree(g_app.d_cur[1]);

@@ -65,6 +65,9 @@ struct rt_device {
     unsigned long long *d_cull_counters = nullptr;  // kCullCounterWords: striped counters + device totals of the cull pass
     uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
     size_t tile_cap = 0, mask_cap = 0;
+    // rt_device_reserve: the geometry the launch buffers are pre-sized for (0: none);
+    // a scene upload re-applies it for the new scene's mask words
+    uint32_t reserve_width = 0, reserve_rows = 0;
     size_t mask_words = 0;  // words the last cull pass wrote (rt_debug_masks)
     // the launch (camera, scene, geometry) the masks / live list / order were made for
     std::vector<uint32_t> tile_key;
@@ -126,6 +129,7 @@ int rt_fail(int code, const char *fmt, ...) {
 extern "C" const char *rt_last_error(void) { return g_err; }
 
 extern "C" int rt_device_create(int hip_device, rt_device **out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!out) return fail(RT_EINVAL, "rt_device_create: out is NULL");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
@@ -197,6 +201,7 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
 }
 
 extern "C" int rt_device_destroy(rt_device *d) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d) return RT_OK;
     (void)hipSetDevice(d->ordinal);
     // the caller's trace stream may already be gone: wait for the whole device
@@ -221,6 +226,8 @@ extern "C" int rt_device_destroy(rt_device *d) {
     delete d;
     return RT_OK;
 }
+
+static int apply_reserve(rt_device *d);  // (rt_device_reserve, below)
 
 // rt_trace is asynchronous on the caller's stream, while uploads go through
 // the device's own non-blocking stream: before a buffer a trace may still
@@ -256,6 +263,7 @@ static bool resolve_counts(rt_device *d, bool wait) {
 }
 
 extern "C" int rt_set_rsqrt_table(rt_device *d, const float table[2048]) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !table) return fail(RT_EINVAL, "rt_set_rsqrt_table: NULL argument");
     HIP_OK(hipSetDevice(d->ordinal));
     if (const int rc = quiesce(d)) return rc;
@@ -431,8 +439,9 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // RTWeekend K/S = 40/4, 28/3, 28/4, 24/4 -> 21.1k/21.9k/21.9k/21.7k (one level
     // at K 40: 19.6k); C5 at 512 spp K/S = 32/4, 24/3, 28/3, 24/2 -> 47.4k/48.2k/
     // 48.3k/48.3k (one level: 46.3k).
-    const char *tl1 = getenv("RT_TWO_LEVEL_W1");  // A/B: one-word tables with two levels (kernel built with RTK_TWO_LEVEL_W1)
-    const bool two_levels = *words >= 2u || (tl1 && tl1[0] == '1');
+    // two levels for tables of two or more mask words only: the kernel walks
+    // one-word tables (at most 32 groups) as one level (rt_kernel.hip clustered_groups)
+    const bool two_levels = *words >= 2u;
     const uint32_t div = two_levels ? (relative ? 17u : 10u) : (relative ? 12u : 8u);
     uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / div));
     if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob
@@ -812,6 +821,7 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
 }
 
 extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
     PackedSet ps[2];
     for (int rs = 0; rs < 2; ++rs) {
@@ -850,7 +860,9 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     d->use_sky = scene->UseSkyColor;
     d->scene_set = true;
     d->scene_gen += 1;
-    return RT_OK;
+    // a reserved geometry keeps its promise for the new scene's mask words (the
+    // device is quiescent here: the upload waited for every launch)
+    return apply_reserve(d);
 }
 
 extern "C" int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p,
@@ -898,8 +910,77 @@ extern "C" int rt_scene_cluster_layout(const rt_scene *scene, uint32_t enable_si
     return RT_OK;
 }
 
+// Launch buffers for n_tiles block tiles (cost, order, live flags, sort
+// scratch, cull counters) and for mask_words cull-mask words.  Growing frees
+// buffers earlier launches may still read, so `sync` (the caller's stream, or
+// the whole device when NULL) is waited for first; growing clears the tile key.
+static int ensure_tile_buffers(rt_device *d, uint32_t n_tiles, hipStream_t sync, bool device_wide) {
+    if (n_tiles <= d->tile_cap && d->d_cull_counters) return RT_OK;
+    if (device_wide) HIP_OK(hipDeviceSynchronize());
+    else HIP_OK(hipStreamSynchronize(sync));
+    if (n_tiles > d->tile_cap) {
+        for (uint32_t **b : {&d->d_tile_cost, &d->d_tile_order, &d->d_tile_scratch, &d->d_tile_live}) {
+            (void)hipFree(*b);
+            *b = nullptr;
+        }
+        d->tile_cap = 0;
+        // cost / order / sort scratch per unit: up to 4 per block tile (wave units)
+        if (hipMalloc(&d->d_tile_cost, 4u * n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_order, 4u * n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(4u * n_tiles)) != hipSuccess)
+            return fail(RT_ENOMEM, "rt_trace: tile order buffers");
+        d->tile_cap = n_tiles;
+        d->last.BufferGrowths += 1;
+    }
+    if (!d->d_cull_counters && hipMalloc(&d->d_cull_counters, kCullCounterWords * 8u) != hipSuccess)
+        return fail(RT_ENOMEM, "rt_trace: tile order buffers");
+    d->tile_key.clear();
+    return RT_OK;
+}
+
+static int ensure_masks(rt_device *d, size_t mask_words, hipStream_t sync, bool device_wide) {
+    if (mask_words <= d->mask_cap) return RT_OK;
+    if (device_wide) HIP_OK(hipDeviceSynchronize());
+    else HIP_OK(hipStreamSynchronize(sync));
+    (void)hipFree(d->d_masks);
+    d->d_masks = nullptr;
+    d->mask_cap = 0;
+    if (hipMalloc(&d->d_masks, mask_words * 8u) != hipSuccess) return fail(RT_ENOMEM, "rt_trace: cull masks");
+    d->mask_cap = mask_words;
+    d->last.BufferGrowths += 1;
+    d->tile_key.clear();
+    return RT_OK;
+}
+
+// The buffers of every launch rt_trace may make at the reserved geometry:
+// the most block tiles over every lanes-per-pixel shape (rt_trace picks P per
+// launch) and the current scene's mask words, so no later launch allocates.
+static int apply_reserve(rt_device *d) {
+    if (!d->reserve_width) return RT_OK;
+    uint32_t n_tiles = 0;
+    for (const int p : {1, 2, 4, 8, 16, 32})
+        n_tiles = std::max(n_tiles, rtk_tile_count(d->reserve_width, d->reserve_rows, p));
+    uint32_t n_words = 1;
+    if (d->scene_set)
+        for (int rs = 0; rs < 2; ++rs) n_words = std::max(n_words, (d->n_groups[rs] + 63u) / 64u);
+    if (const int rc = ensure_tile_buffers(d, n_tiles, nullptr, true)) return rc;
+    return ensure_masks(d, (size_t)n_tiles * 4u * n_words, nullptr, true);
+}
+
+extern "C" int rt_device_reserve(rt_device *d, uint32_t width, uint32_t local_rows) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    if (!d || width == 0 || local_rows == 0 || width > 65536 || local_rows > 65536)
+        return fail(RT_EINVAL, "rt_device_reserve: bad argument");
+    HIP_OK(hipSetDevice(d->ordinal));
+    d->reserve_width = std::max(d->reserve_width, width);
+    d->reserve_rows = std::max(d->reserve_rows, local_rows);
+    return apply_reserve(d);
+}
+
 extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
                         void *stream) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !cam || !desc || !d_rays) return fail(RT_EINVAL, "rt_trace: NULL argument");
     if (!d->lut_set) return fail(RT_EINVAL, "rt_trace: rsqrt table not set (rt_set_rsqrt_table)");
     if (!d->scene_set) return fail(RT_EINVAL, "rt_trace: no scene uploaded (rt_scene_upload)");
@@ -1057,32 +1138,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         d->tile_stream = s;
         d->tile_stream_set = true;
     }
-    if (n_tiles > d->tile_cap) {
-        HIP_OK(hipStreamSynchronize(s));
-        for (uint32_t **b : {&d->d_tile_cost, &d->d_tile_order, &d->d_tile_scratch, &d->d_tile_live}) {
-            (void)hipFree(*b);
-            *b = nullptr;
-        }
-        // cost / order / sort scratch per unit: up to 4 per block tile (wave units)
-        if (hipMalloc(&d->d_tile_cost, 4u * n_tiles * 4u) != hipSuccess ||
-            hipMalloc(&d->d_tile_order, 4u * n_tiles * 4u) != hipSuccess ||
-            hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
-            hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(4u * n_tiles)) != hipSuccess)
-            return fail(RT_ENOMEM, "rt_trace: tile order buffers");
-        if (!d->d_cull_counters && hipMalloc(&d->d_cull_counters, kCullCounterWords * 8u) != hipSuccess)
-            return fail(RT_ENOMEM, "rt_trace: tile order buffers");
-        d->tile_cap = n_tiles;
-        d->tile_key.clear();
-    }
+    // (no allocation here once rt_device_reserve has sized the buffers for this geometry)
+    if (const int rc = ensure_tile_buffers(d, n_tiles, s, false)) return rc;
     const size_t mask_words = (size_t)n_tiles * 4u * n_words;
-    if (cull && mask_words > d->mask_cap) {
-        HIP_OK(hipStreamSynchronize(s));
-        (void)hipFree(d->d_masks);
-        d->d_masks = nullptr;
-        if (hipMalloc(&d->d_masks, mask_words * 8u) != hipSuccess) return fail(RT_ENOMEM, "rt_trace: cull masks");
-        d->mask_cap = mask_words;
-        d->tile_key.clear();
-    }
+    if (cull)
+        if (const int rc = ensure_masks(d, mask_words, s, false)) return rc;
     const bool new_key = key != d->tile_key;
     uint32_t head_frames = 0;  // > 0: split this launch (first launch of a key, below): frames of the leading parts
     uint32_t split[8], n_split = 0;
@@ -1206,6 +1266,7 @@ extern "C" int rt_encode_rgba8(const float *d_accum_v4, uint32_t *d_rgba8, uint6
 }
 
 extern "C" int rt_trace_last_info(rt_device *d, rt_trace_info *out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !out) return fail(RT_EINVAL, "rt_trace_last_info: NULL argument");
     // the live/dead totals of the last launch's key: waits for them if they
     // are still on their way from the device (the only blocking part)
@@ -1220,12 +1281,14 @@ extern "C" int rt_trace_last_info(rt_device *d, rt_trace_info *out) {
 }
 
 extern "C" int rt_device_synchronize(rt_device *d) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d) return fail(RT_EINVAL, "rt_device_synchronize: NULL device");
     HIP_OK(hipSetDevice(d->ordinal));
     return quiesce(d);
 }
 
 extern "C" int rt_debug_stats(rt_device *d, uint64_t out[32], int reset) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !out) return fail(RT_EINVAL, "rt_debug_stats: NULL argument");
     memset(out, 0, 32 * sizeof(uint64_t));
     if (!d->d_stats) return 0;
@@ -1237,6 +1300,7 @@ extern "C" int rt_debug_stats(rt_device *d, uint64_t out[32], int reset) {
 }
 
 extern "C" int64_t rt_debug_masks(rt_device *d, uint64_t *out, uint64_t max_words) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !out) return fail(RT_EINVAL, "rt_debug_masks: NULL argument");
     if (!d->d_masks || d->tile_key.empty() || !d->mask_words) return 0;
     const uint64_t n = max_words < d->mask_words ? max_words : d->mask_words;
@@ -1247,6 +1311,7 @@ extern "C" int64_t rt_debug_masks(rt_device *d, uint64_t *out, uint64_t max_word
 }
 
 extern "C" int64_t rt_debug_wave_times(rt_device *d, uint64_t *out, uint64_t max_waves) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!d || !out) return fail(RT_EINVAL, "rt_debug_wave_times: NULL argument");
     if (!d->d_wave_times) return 0;
     const uint64_t n = max_waves < d->wave_times_cap ? max_waves : d->wave_times_cap;

@@ -151,6 +151,23 @@ extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const u
                                 const unsigned long long *dead_pixels, hipStream_t stream);
 // dst[0] += sum of slots[0, n) (the gathered per-device ray counters)
 extern "C" int rtk_launch_sum_u64(const uint64_t *slots, uint32_t n, uint64_t *dst, hipStream_t stream);
+// Restores the caller's current HIP device when a C-ABI entry point returns:
+// entry points switch to their device's ordinal (hipSetDevice), and the
+// caller's own HIP work must keep targeting the device it had selected.
+struct DeviceGuard {
+    int saved = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&saved) != hipSuccess) {
+            saved = -1;
+            (void)hipGetLastError();
+        }
+    }
+    ~DeviceGuard() {
+        if (saved >= 0) (void)hipSetDevice(saved);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
 // sets rt_last_error()'s text and returns `code` (rt_host.cpp)
 int rt_fail(int code, const char *fmt, ...);
 extern "C" int rtk_launch_encode(const void *accum, void *out, uint64_t n, uint32_t pow_mode, hipStream_t stream);

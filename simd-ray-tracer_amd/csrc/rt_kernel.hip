@@ -601,18 +601,6 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
 // own estimate cleared the pair has a proven miss there, which its exact test
 // reproduces, so no per-lane flags are needed.
 constexpr int kClWords = 4;  // pair-mask words (n_groups <= 128)
-#ifndef RTK_MEMBER_BEHIND  // 1: member pairs of scene-wide tables also take the behind-origin test (A/B)
-#define RTK_MEMBER_BEHIND 1
-#endif
-#ifndef RTK_MEMBER_BEHIND_REL  // the same for per-lane (REL) tables (A/B)
-#define RTK_MEMBER_BEHIND_REL 0
-#endif
-#ifndef RTK_SUB_SLAB  // 1: sub-clusters of per-lane tables run the height-slab test too (A/B)
-#define RTK_SUB_SLAB 1
-#endif
-#ifndef RTK_TWO_LEVEL_W1  // 1: one-word cluster tables walk two levels too (A/B; the host needs RT_TWO_LEVEL_W1=1)
-#define RTK_TWO_LEVEL_W1 0
-#endif
 // Per-lane thresholds (pf_relative, rt_host.cpp cluster_table "relative"):
 // cluster: e_c >= RN(cc kClRel + R_c); sphere: e >= RN(cc kPfRel + r^2) (kPfRel
 // below); behind: T < RN(b - cc kBehindRel).
@@ -692,7 +680,7 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         // threshold is a per-lane FMA, and the rule stays at the cluster level
         // (RTWeekend +2.7 % same box; C2's scene-wide table loses 1.7 % without it).
         // Either way a skipped pair is a proven miss.
-        constexpr bool kBehind = REL ? RTK_MEMBER_BEHIND_REL != 0 : RTK_MEMBER_BEHIND != 0;
+        constexpr bool kBehind = !REL;
         const uint64_t f0m = kBehind ? ballot_and(!(v.x >= t0), !(T.x < b0)) : __builtin_amdgcn_ballot_w64(!(v.x >= t0));
         const uint64_t f1m = kBehind ? ballot_and(!(v.y >= t1), !(T.y < b1)) : __builtin_amdgcn_ballot_w64(!(v.y >= t1));
         const bool f0 = f0m != 0, f1 = f1m != 0;
@@ -757,7 +745,7 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
     cv4f_t *ct = (cv4f_t *)a.clusters;
     uint64_t wave[kClWords] = {0ull, 0ull, 0ull, 0ull};
     constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W, REL);
-    constexpr bool kTwoLevels = W >= 2 || RTK_TWO_LEVEL_W1;  // (W = 1: A/B build, host RT_TWO_LEVEL_W1=1)
+    constexpr bool kTwoLevels = W >= 2;
     // per-lane part of the height-slab margin (REL tables; rt_host.cpp cluster_table)
     const float oy = ray.y.x, dy = ray.y.y;
     const float slab_e0 = REL ? __builtin_fmaf(__builtin_fabsf(oy), 0x1p-21f, kSlabRel) : 0.0f;
@@ -773,7 +761,7 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         for (uint32_t off = first * kEntryBytes, end = (first + count) * kEntryBytes; off != end; off += kEntryBytes) {
             cv4f_t *e = cl_entry(ct, off);
             uint64_t m0, m1;
-            cluster_pair<REL, RTK_SUB_SLAB != 0>(e, ray, oy, dy, slab_e0, m0, m1);
+            cluster_pair<REL>(e, ray, oy, dy, slab_e0, m0, m1);
             members(e, m0 != 0, m1 != 0);
         }
     };
@@ -913,22 +901,6 @@ constexpr bool kStats = false;
 #endif
 
 constexpr int kWavesPerBlock = 4;
-#ifndef RTK_FOLD_BEFORE_PRIMARY  // 1: the owner folds its ring only before primary rounds (A/B)
-#define RTK_FOLD_BEFORE_PRIMARY 1
-#endif
-constexpr bool kFoldBeforePrimary = RTK_FOLD_BEFORE_PRIMARY != 0;
-#ifndef RTK_FOLD_LAZY  // 1: ... and only when a lane waits for ring space (A/B)
-#define RTK_FOLD_LAZY 1
-#endif
-constexpr bool kFoldLazy = RTK_FOLD_LAZY != 0;
-// 1: a secondary round shades nothing.  Its hits wait (lane mode 3, the hit
-// parked in LDS) and are shaded by the next primary round's shading block,
-// which runs anyway for that round's own hits: about one secondary ray in five
-// hits, so a secondary round's shading block ran at ~1/5 lane utilisation.
-#ifndef RTK_DEFER_SHADE
-#define RTK_DEFER_SHADE 0
-#endif
-constexpr bool kDeferShade = RTK_DEFER_SHADE != 0;
 // primary group mask words per wave tile: the LDS-image kernels keep this
 // small (it is static LDS, and C2's blocks fill the CU's 160 KB 7 times)
 template <bool GS>
@@ -937,28 +909,12 @@ struct MaskWords {
 };
 constexpr uint32_t kFoldTable = 256;
 // Per-pixel out-of-order sample slots (LDS ring): at least P (every sample
-// lane holds one sample in flight) plus slack.
-#ifndef RTK_RING_SMALL_P  // ring slots per pixel for P <= 4 (A/B)
-#define RTK_RING_SMALL_P 16
-#endif
-#ifndef RTK_FOLD3  // 1: three lanes of a pixel fold one colour channel each (P >= 4; A/B)
-#define RTK_FOLD3 1
-#endif
-#ifndef RTK_FOLD_FRONTIER  // 1: ring readiness from the lanes' sample cursors, not per-slot flags (A/B)
-#define RTK_FOLD_FRONTIER 1
-#endif
-#ifndef RTK_FOLD_WHOLE  // 1: the frontier fold takes whole aligned batches of four, no per-slot selects (A/B)
-#define RTK_FOLD_WHOLE 1
-#endif
-#ifndef RTK_FOLD_BATCH_SMALL_P  // ring slots the owner reads per LDS round trip at P <= 4 (A/B)
-#define RTK_FOLD_BATCH_SMALL_P 2
-#endif
-#ifndef RTK_RING_PER_LANE  // ring slots per sample lane for P > 4 (A/B)
-#define RTK_RING_PER_LANE 2
-#endif
+// lane holds one sample in flight) plus slack: 16 per pixel at P <= 4 (12 and
+// 32 measured slower), 2 per sample lane above.  A multiple of 4, so a
+// whole-batch fold never wraps.
 template <int P>
 struct Ring {
-    static constexpr uint32_t N = P <= 4 ? (uint32_t)RTK_RING_SMALL_P : (uint32_t)RTK_RING_PER_LANE * (uint32_t)P;
+    static constexpr uint32_t N = P <= 4 ? 16u : 2u * (uint32_t)P;
 };
 
 #ifndef RTK_SOLO_WAVES_PER_SIMD  // the same target for the one-wave kernels (A/B: make variant KFLAGS=-DRTK_SOLO_WAVES_PER_SIMD=8)
@@ -1040,9 +996,6 @@ void trace_kernel(TraceArgs a) {
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
     __shared__ float4 s_ring[P > 1 ? kWB * kRing * kRingStride : 1];
-    // a hit found by a secondary round waits here (mode 3) for the next primary
-    // round's shading block: {tmin, sphere index | inside << 31}, lane-private
-    __shared__ float2 s_hit[kDeferShade ? kWB * 64u : 1u];
     const uint32_t lut_f4 = a.lut_in_lds ? 512u : 0u;  // see rtk_lds_bytes
     const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, a.lut_in_lds != 0u};
     float2 *fold = reinterpret_cast<float2 *>(smem + lut_f4);
@@ -1065,9 +1018,6 @@ void trace_kernel(TraceArgs a) {
             const uint32_t pc = a.prev_count + i;
             fold[i] = make_float2(1.0f / (float)(pc + 1u), (float)pc / (float)(pc + 1u));
         }
-        if (P > 1 && !RTK_FOLD_FRONTIER)  // (the flag protocol needs clear flags; the frontier reads only parked slots)
-            for (uint32_t i = threadIdx.x; i < kWB * kRing * kRingStride; i += blockDim.x)
-                s_ring[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 
     // wave: quadrant of the block tile; sw: the wave's LDS slot in its workgroup
@@ -1107,15 +1057,14 @@ void trace_kernel(TraceArgs a) {
     // wave folds 3 chains per pixel at once (at P = 16 the owner's three-channel
     // fold was ~15 % of the wave's VALU instructions).  The owner gathers the
     // other two channels by DPP for the final store.
-    constexpr bool FOLD3 = RTK_FOLD3 != 0 && P >= 4;
+    constexpr bool FOLD3 = P >= 4;
     const bool folder = FOLD3 ? j < 3u : owner;
     // the channel a lane reads from a ring slot (lanes j >= 3 of the whole-batch fold
     // read the ratio word and discard their sums)
     const uint32_t jc = j < 3u ? j : 3u;
     // every lane of a pixel keeps the fold cursor (whole-batch frontier fold)
-    constexpr bool kCursorPerLane = RTK_FOLD_FRONTIER && RTK_FOLD_WHOLE && P > 1;
+    constexpr bool kCursorPerLane = P > 1;
     float4 *ring = s_ring + sw * kRing * kRingStride + pl;
-    float2 *hit_slot = s_hit + (kDeferShade ? sw * 64u + lane : 0u);
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     // the wave tile's primary group mask, from the cull pass (rtk_launch_cull)
@@ -1138,8 +1087,7 @@ void trace_kernel(TraceArgs a) {
 
     // owner lanes of in-image pixels (they fold until every frame is folded)
     const uint64_t folding = ballot_and(owner, valid);
-    // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left,
-    // 3 = a secondary round's hit waits to be shaded (kDeferShade)
+    // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left
     uint32_t k = j;            // this lane's next (or current) sample
     uint32_t folded = 0;       // owner: samples folded so far
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
@@ -1235,124 +1183,59 @@ void trace_kernel(TraceArgs a) {
         return min(f, a.frames);
     };
     auto fold_ring = [&]() {
-        if (RTK_FOLD_FRONTIER && P > 1) {
-            // ---- running-mean blend (main.cpp:484-489) of every parked sample, in
-            // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
-            // sample's lane.  Slots [folded, F) are all parked: no per-slot flags, no
-            // clearing writes.  Batches of four slots aligned to 4 (kRing is a multiple
-            // of 4, so a batch never wraps; its LDS reads take immediate offsets).
-            const uint32_t F = parked_frontier();
-            if (RTK_FOLD_WHOLE && valid) {
-                // Whole aligned batches only (folded stays a multiple of 4), each slot
-                // folded straight with no per-slot test; the ragged end once every
-                // sample is parked.  A lane that waits for ring space still gets it: the
-                // lane holding the frontier sample F < folded + 4 <= folded + kRing
-                // is never blocked, so the frontier keeps moving.  Every lane of the
-                // pixel runs the loop (F is uniform over them), so each keeps the fold
-                // cursor itself; only the folding lanes' sums are used.
-                const uint32_t Fb = F >= a.frames ? F : (F & ~3u);
-                while (folded + 4u <= Fb) {
-                    const float4 *base = ring + (folded % kRing) * kRingStride;
-                    float v[4], w[4];
-                    float4 r4[4];
+        if (P == 1) return;
+        // ---- running-mean blend (main.cpp:484-489) of every parked sample, in
+        // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
+        // sample's lane.  Slots [folded, F) are all parked: no per-slot flags, no
+        // clearing writes.  Whole batches of four slots aligned to 4 (kRing is a
+        // multiple of 4, so a batch never wraps; its LDS reads take immediate
+        // offsets), each slot folded straight with no per-slot test; the ragged end
+        // once every sample is parked.  A lane that waits for ring space still gets
+        // it: the lane holding the frontier sample F < folded + 4 <= folded + kRing
+        // is never blocked, so the frontier keeps moving.  Every lane of the pixel
+        // runs the loop (F is uniform over them), so each keeps the fold cursor
+        // itself; only the folding lanes' sums are used.
+        const uint32_t F = parked_frontier();  // (every lane active: a DPP reduction)
+        if (!valid) return;
+        const uint32_t Fb = F >= a.frames ? F : (F & ~3u);
+        while (folded + 4u <= Fb) {
+            const float4 *base = ring + (folded % kRing) * kRingStride;
+            float v[4], w[4];
+            float4 r4[4];
 #pragma unroll
-                    for (uint32_t i = 0; i < 4u; ++i) {
-                        if (FOLD3) {
-                            const float *slot = reinterpret_cast<const float *>(base + i * kRingStride);
-                            v[i] = slot[jc];
-                            w[i] = slot[3];
-                        } else {
-                            r4[i] = base[i * kRingStride];
-                        }
-                    }
-#pragma unroll
-                    for (uint32_t i = 0; i < 4u; ++i) {
-                        if (FOLD3) {
-                            accx = v[i] + accx * -w[i];
-                        } else {
-                            accx = r4[i].x + accx * -r4[i].w;
-                            accy = r4[i].y + accy * -r4[i].w;
-                            accz = r4[i].z + accz * -r4[i].w;
-                        }
-                    }
-                    folded += 4u;
-                }
-                while (folded < Fb) {
-                    const float4 *s4 = ring + (folded % kRing) * kRingStride;
-                    if (FOLD3) {
-                        const float *slot = reinterpret_cast<const float *>(s4);
-                        accx = slot[jc] + accx * -slot[3];
-                    } else {
-                        const float4 r = *s4;
-                        accx = r.x + accx * -r.w;
-                        accy = r.y + accy * -r.w;
-                        accz = r.z + accz * -r.w;
-                    }
-                    folded += 1u;
-                }
-            } else if (folder && valid) {
-                while (folded < F) {
-                    const uint32_t a0 = folded & ~3u;
-                    const float4 *base = ring + (a0 % kRing) * kRingStride;
-                    float v[4], w[4];
-                    float4 r4[4];
-#pragma unroll
-                    for (uint32_t i = 0; i < 4u; ++i) {
-                        if (FOLD3) {  // this lane's channel j and the ratio
-                            const float *slot = reinterpret_cast<const float *>(base + i * kRingStride);
-                            v[i] = slot[j];
-                            w[i] = slot[3];
-                        } else {
-                            r4[i] = base[i * kRingStride];
-                        }
-                    }
-#pragma unroll
-                    for (uint32_t i = 0; i < 4u; ++i) {
-                        const bool take = a0 + i >= folded && a0 + i < F;
-                        if (FOLD3) {
-                            const float t = v[i] + accx * -w[i];
-                            accx = take ? t : accx;
-                        } else {
-                            const float tx = r4[i].x + accx * -r4[i].w;
-                            const float ty = r4[i].y + accy * -r4[i].w;
-                            const float tz = r4[i].z + accz * -r4[i].w;
-                            accx = take ? tx : accx;
-                            accy = take ? ty : accy;
-                            accz = take ? tz : accz;
-                        }
-                    }
-                    folded = min(a0 + 4u, F);
+            for (uint32_t i = 0; i < 4u; ++i) {
+                if (FOLD3) {
+                    const float *slot = reinterpret_cast<const float *>(base + i * kRingStride);
+                    v[i] = slot[jc];
+                    w[i] = slot[3];
+                } else {
+                    r4[i] = base[i * kRingStride];
                 }
             }
-        } else if (P > 1 && folder && valid) {
-            // ---- running-mean blend (main.cpp:484-489) of every finished sample, in
-            // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
-            // sample's lane.  The fold is one sequential chain per pixel, so the owner
-            // reads kFoldBatch ring slots per LDS round trip (more for more lanes).
-            constexpr uint32_t kFoldBatch = P >= 8 ? 4u : (uint32_t)RTK_FOLD_BATCH_SMALL_P;
-            bool more = true;
-            while (more && folded < a.frames) {
-                float4 r[kFoldBatch];
 #pragma unroll
-                for (uint32_t i = 0; i < kFoldBatch; ++i) r[i] = ring[((folded + i) % kRing) * kRingStride];
-#pragma unroll
-                for (uint32_t i = 0; i < kFoldBatch; ++i) {
-                    more = more && folded < a.frames && __builtin_signbit(r[i].w);
-                    if (more) {
-                        if (FOLD3) {  // (lanes 1 and 2 read .w in this batch before lane 0 clears it)
-                            const float v = j == 0u ? r[i].x : j == 1u ? r[i].y : r[i].z;
-                            accx = v + accx * -r[i].w;
-                            if (owner) ring[(folded % kRing) * kRingStride].w = 0.0f;
-                        } else {
-                            accx = r[i].x + accx * -r[i].w;
-                            accy = r[i].y + accy * -r[i].w;
-                            accz = r[i].z + accz * -r[i].w;
-                            ring[(folded % kRing) * kRingStride].w = 0.0f;
-                        }
-                        folded += 1u;
-                    }
+            for (uint32_t i = 0; i < 4u; ++i) {
+                if (FOLD3) {
+                    accx = v[i] + accx * -w[i];
+                } else {
+                    accx = r4[i].x + accx * -r4[i].w;
+                    accy = r4[i].y + accy * -r4[i].w;
+                    accz = r4[i].z + accz * -r4[i].w;
                 }
             }
+            folded += 4u;
+        }
+        while (folded < Fb) {
+            const float4 *s4 = ring + (folded % kRing) * kRingStride;
+            if (FOLD3) {
+                const float *slot = reinterpret_cast<const float *>(s4);
+                accx = slot[jc] + accx * -slot[3];
+            } else {
+                const float4 r = *s4;
+                accx = r.x + accx * -r.w;
+                accy = r.y + accy * -r.w;
+                accz = r.z + accz * -r.w;
+            }
+            folded += 1u;
         }
     };
     for (;;) {
@@ -1365,27 +1248,26 @@ void trace_kernel(TraceArgs a) {
         bool can_start = mode == 0u && ring_ok;
         uint64_t pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         const uint64_t sec = __builtin_amdgcn_ballot_w64(mode == 1u);
-        // hits parked by a secondary round, shaded by the next non-secondary round
-        const uint64_t shd = kDeferShade ? __builtin_amdgcn_ballot_w64(mode == 3u) : 0ull;
         const uint64_t alive = __builtin_amdgcn_ballot_w64(mode != 2u) | (folding & __builtin_amdgcn_ballot_w64(folded < a.frames));
         if (alive == 0) break;
         const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
         // Secondary segments run the full sphere loop; let them gather until
         // enough lanes share one (or no primary work is ready).
-        const bool do_sec = sec != 0 && ((pri | shd) == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
         // (lazy: only when some lane waits for ring space, or nothing else is left)
-        const bool fold_now = !do_sec && (!kFoldLazy || (pri | sec | shd) == 0 ||
-                                          (__builtin_amdgcn_ballot_w64(mode == 0u) & ~pri) != 0);
-        if (kFoldBeforePrimary && fold_now) {
+        const bool fold_now = !do_sec && ((pri | sec) == 0 || (__builtin_amdgcn_ballot_w64(mode == 0u) & ~pri) != 0);
+        if (fold_now) {
             // the owners fold only before a primary round (or when nothing is left to
             // trace): a secondary round starts no sample, so it needs no ring space
+            const uint64_t st_f0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
             fold_ring();
+            if (kStats && a.stats) st_cyc_fold += __builtin_amdgcn_s_memtime() - st_f0;
             folded_g = fold_cursor();
             ring_ok = P == 1 || k < folded_g + kRing;
             can_start = mode == 0u && ring_ok;
             pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         }
-        if ((pri | sec | shd) != 0) {
+        if ((pri | sec) != 0) {
             if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
                 if (do_sec && __builtin_popcountll(sec) < 16) { st_sparse_it += 1; st_sparse_lanes += __builtin_popcountll(sec); }
@@ -1407,23 +1289,18 @@ void trace_kernel(TraceArgs a) {
             }
             // do_sec ? mode == 1 : can_start, as one compare against a uniform mode
             // and a uniform override of the ring test (no lane-mask select)
-            // (a parked lane's segment was counted by the round that traced it)
-            const bool parked = kDeferShade && !do_sec && mode == 3u;
-            const bool traces = kDeferShade ? (do_sec ? mode == 1u : (mode == 0u && ring_ok) || mode == 3u)
-                                            : mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
+            const bool traces = mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
             if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
             if (traces) {
-                if (!do_sec && !parked) start_sample(kernel_args(), x, y, a.prev_count + k, p);
-                bool done, defer = false;
+                if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
+                bool done;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
                 } else {
                     Hit h;
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
-                    if (parked) {
-                        // nothing to trace: the hit comes from the LDS slot below
-                    } else if (CULL && !do_sec) {
+                    if (CULL && !do_sec) {
                         for (uint32_t w = 0; w < n_words; ++w) {
                             // (readfirstlane returns int: widen each half as u32, or
                             // bit 31 would sign-extend into groups 32..63)
@@ -1503,17 +1380,7 @@ void trace_kernel(TraceArgs a) {
                         sidx = h.g0;
                         inside = h.ins != 0;
                     }
-                    if (parked) {
-                        const float2 hs = *hit_slot;
-                        tmin = hs.x;
-                        sidx = __float_as_uint(hs.y) & 0x7FFFFFFFu;
-                        inside = (__float_as_uint(hs.y) >> 31) != 0u;
-                    }
-                    if (kDeferShade && do_sec && tmin != kFMax) {
-                        *hit_slot = make_float2(tmin, __uint_as_float(sidx | (inside ? 0x80000000u : 0u)));
-                        defer = true;
-                        done = false;
-                    } else if (tmin == kFMax) {
+                    if (tmin == kFMax) {
                         if (a.use_sky) {  // main.cpp:434-438
                             const float s = (p.ry.y + 1.0f) * 0.5f;
                             const float w = (1.0f - s) * 1.0f;
@@ -1549,17 +1416,15 @@ void trace_kernel(TraceArgs a) {
                     k += P;
                     mode = k < a.frames ? 0u : 2u;
                 } else {
-                    mode = defer ? 3u : 1u;
+                    mode = 1u;
                 }
             }
         }
         const uint64_t st_t1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
-        if (kStats && a.stats && (pri | sec | shd) != 0) {
-            const bool was_sec = sec != 0 && ((pri | shd) == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        if (kStats && a.stats && (pri | sec) != 0) {
+            const bool was_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
             (was_sec ? st_cyc_sec : st_cyc_pri) += st_t1 - st_t0;
         }
-        if (!kFoldBeforePrimary) fold_ring();
-        if (kStats && a.stats) st_cyc_fold += __builtin_amdgcn_s_memtime() - st_t1;
     }
 
     if (FOLD3) {  // channels 1 and 2 from lanes j = 1, 2 of the pixel's quad (quad_perm 1,1,1,1 / 2,2,2,2)

@@ -132,6 +132,9 @@ struct rt_multi {
     uint64_t *ray_slots = nullptr;
     hipStream_t gather = nullptr;  // devices[0]
     hipEvent_t start = nullptr, gathered = nullptr;
+    // timing of the gather: from every trace done (the gather stream has waited
+    // for each device's traced event) to the frame assembled on devices[0]
+    hipEvent_t g0[kSlots] = {}, g1[kSlots] = {};
     hipEvent_t copied[kSlots] = {};   // peer transport: slot b's copies are done (slot b free again)
     bool slot_used[kSlots] = {};      // slot b has been gathered before (its free event is valid)
     uint32_t calls = 0;               // rt_multi_trace calls (slot = calls & 1)
@@ -163,6 +166,7 @@ static void destroy_shard(Shard &sh) {
 }
 
 extern "C" int rt_multi_destroy(rt_multi *m) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m) return RT_OK;
     for (Shard &sh : m->s) {
         (void)hipSetDevice(sh.ordinal);
@@ -175,7 +179,7 @@ extern "C" int rt_multi_destroy(rt_multi *m) {
         (void)hipFree(m->stage_cur);
         (void)hipFree(m->stage_prev);
         (void)hipFree(m->ray_slots);
-        for (hipEvent_t e : {m->start, m->gathered, m->copied[0], m->copied[1]})
+        for (hipEvent_t e : {m->start, m->gathered, m->copied[0], m->copied[1], m->g0[0], m->g0[1], m->g1[0], m->g1[1]})
             if (e) (void)hipEventDestroy(e);
         if (m->gather) (void)hipStreamDestroy(m->gather);
     }
@@ -185,6 +189,7 @@ extern "C" int rt_multi_destroy(rt_multi *m) {
 }
 
 extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t transport, rt_multi **out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!hip_devices || !out || count == 0 || count > RT_MULTI_MAX_DEVICES)
         return rt_fail(RT_EINVAL, "rt_multi_create: need 1..%u devices", RT_MULTI_MAX_DEVICES);
     if (transport > RT_MULTI_PEER) return rt_fail(RT_EINVAL, "rt_multi_create: unknown transport %u", transport);
@@ -218,6 +223,8 @@ extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t 
         hipEventCreateWithFlags(&m->gathered, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->copied[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&m->copied[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&m->g0[0]) != hipSuccess || hipEventCreate(&m->g0[1]) != hipSuccess ||
+        hipEventCreate(&m->g1[0]) != hipSuccess || hipEventCreate(&m->g1[1]) != hipSuccess ||
         hipMalloc(&m->ray_slots, RT_MULTI_MAX_DEVICES * sizeof(uint64_t)) != hipSuccess) {
         rt_multi_destroy(m);
         return rt_fail(RT_ENOMEM, "rt_multi_create: gather resources on device %d", d0);
@@ -257,6 +264,7 @@ extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t 
 }
 
 extern "C" int rt_multi_set_rsqrt_table(rt_multi *m, const float table[2048]) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m || !table) return rt_fail(RT_EINVAL, "rt_multi_set_rsqrt_table: NULL argument");
     if (const int rc = rt_multi_synchronize(m)) return rc;
     for (Shard &sh : m->s)
@@ -265,6 +273,7 @@ extern "C" int rt_multi_set_rsqrt_table(rt_multi *m, const float table[2048]) {
 }
 
 extern "C" int rt_multi_scene_upload(rt_multi *m, const rt_scene *scene) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m || !scene) return rt_fail(RT_EINVAL, "rt_multi_scene_upload: NULL argument");
     if (const int rc = rt_multi_synchronize(m)) return rc;
     for (Shard &sh : m->s)
@@ -273,6 +282,7 @@ extern "C" int rt_multi_scene_upload(rt_multi *m, const rt_scene *scene) {
 }
 
 extern "C" int rt_multi_synchronize(rt_multi *m) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m) return rt_fail(RT_EINVAL, "rt_multi_synchronize: NULL argument");
     for (Shard &sh : m->s) {
         MHIP(hipSetDevice(sh.ordinal));
@@ -286,6 +296,7 @@ extern "C" int rt_multi_synchronize(rt_multi *m) {
 }
 
 extern "C" int rt_multi_get_info(rt_multi *m, rt_multi_info *out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m || !out) return rt_fail(RT_EINVAL, "rt_multi_get_info: NULL argument");
     out->DeviceCount = (uint32_t)m->s.size();
     out->Transport = m->transport;
@@ -305,6 +316,7 @@ extern "C" int rt_multi_get_info(rt_multi *m, rt_multi_info *out) {
 }
 
 extern "C" int rt_multi_last_trace_ms(rt_multi *m, float *ms_out, uint32_t count) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m || !ms_out || count < m->s.size()) return rt_fail(RT_EINVAL, "rt_multi_last_trace_ms: bad argument");
     if (m->calls == 0) return rt_fail(RT_EINVAL, "rt_multi_last_trace_ms: no call yet");
     const uint32_t b = m->last_slot;
@@ -317,11 +329,56 @@ extern "C" int rt_multi_last_trace_ms(rt_multi *m, float *ms_out, uint32_t count
     return RT_OK;
 }
 
+extern "C" int rt_multi_last_gather_ms(rt_multi *m, float *ms_out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    if (!m || !ms_out) return rt_fail(RT_EINVAL, "rt_multi_last_gather_ms: NULL argument");
+    if (m->calls == 0) return rt_fail(RT_EINVAL, "rt_multi_last_gather_ms: no call yet");
+    MHIP(hipSetDevice(m->s[0].ordinal));
+    MHIP(hipEventSynchronize(m->g1[m->last_slot]));
+    MHIP(hipEventElapsedTime(ms_out, m->g0[m->last_slot], m->g1[m->last_slot]));
+    return RT_OK;
+}
+
+extern "C" int rt_multi_shard_info(rt_multi *m, uint32_t index, rt_trace_info *out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    if (!m || !out || index >= m->s.size()) return rt_fail(RT_EINVAL, "rt_multi_shard_info: bad argument");
+    if (!m->s[index].launched) return rt_fail(RT_EINVAL, "rt_multi_shard_info: device %u traced nothing in the last call", index);
+    return rt_trace_last_info(m->s[index].dev, out);
+}
+
+extern "C" int rt_multi_reserve(rt_multi *m, uint32_t width, uint32_t height, uint32_t band_rows, uint32_t flags) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    const uint32_t R = band_rows ? band_rows : 8u;
+    if (!m || width == 0 || height == 0 || width > 65536 || height > 65536 || R % 8u ||
+        (flags & ~RT_MULTI_RESERVE_MEAN))
+        return rt_fail(RT_EINVAL, "rt_multi_reserve: bad argument");
+    if (const int rc = rt_multi_synchronize(m)) return rc;  // growing frees buffers in-flight calls may use
+    const uint32_t n = (uint32_t)m->s.size();
+    const uint32_t maxr = max_local_rows(height, R, n);
+    for (Shard &sh : m->s) {
+        MHIP(hipSetDevice(sh.ordinal));
+        if (const int rc = grow(&sh.prev, &sh.cap_prev, (size_t)maxr * width * 16u)) return rc;
+        size_t cap = sh.cap_cur;
+        for (int b = 0; b < kSlots; ++b) {
+            cap = sh.cap_cur;
+            if (const int rc = grow(&sh.cur[b], &cap, (size_t)maxr * width * 4u)) return rc;
+        }
+        sh.cap_cur = cap;
+        if (const int rc = rt_device_reserve(sh.dev, width, maxr)) return rc;
+    }
+    MHIP(hipSetDevice(m->s[0].ordinal));
+    if (const int rc = grow(&m->stage_cur, &m->cap_stage_cur, (size_t)n * maxr * width * 4u)) return rc;
+    if (flags & RT_MULTI_RESERVE_MEAN)
+        if (const int rc = grow(&m->stage_prev, &m->cap_stage_prev, (size_t)n * maxr * width * 16u)) return rc;
+    return RT_OK;
+}
+
 static int multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
                        hipStream_t caller, bool restart, bool same_geometry);
 
 extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_desc *desc, uint64_t *d_rays,
                               void *stream) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!m || !cam || !desc || !d_rays) return rt_fail(RT_EINVAL, "rt_multi_trace: NULL argument");
     if (desc->BandCount != 0 || desc->BandIndex != 0)
         return rt_fail(RT_EINVAL, "rt_multi_trace: BandCount/BandIndex must be 0 (bands are dealt over the devices)");
@@ -345,8 +402,11 @@ extern "C" int rt_multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_t
         return rc;
     }
     if (restart) {
+        // the frames were folded with the weights of PreviousRayCount + k (an
+        // ACCUM_ZERO launch may start at any count), so a continuation names
+        // PreviousRayCount + Frames, exactly as for one device's rt_trace
         m->accum_valid = desc->Frames > 0;
-        m->resident_frames = desc->Frames;
+        m->resident_frames = (uint64_t)desc->PreviousRayCount + desc->Frames;
     } else {
         m->resident_frames += desc->Frames;
     }
@@ -428,6 +488,9 @@ static int multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_de
             MHIP(hipSetDevice(sh.ordinal));
             MHIP(hipStreamWaitEvent(sh.xfer, sh.traced[b], 0));
         }
+        MHIP(hipSetDevice(d0));
+        for (Shard &sh : m->s) MHIP(hipStreamWaitEvent(m->gather, sh.traced[b], 0));
+        MHIP(hipEventRecord(m->g0[b], m->gather));
         const Rccl &r = rccl();
         NCCL_OK(r.GroupStart());
         for (uint32_t i = 0; i < n; ++i) {
@@ -452,9 +515,10 @@ static int multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_de
         MHIP(hipSetDevice(d0));
     } else {
         MHIP(hipSetDevice(d0));
+        for (Shard &sh : m->s) MHIP(hipStreamWaitEvent(m->gather, sh.traced[b], 0));
+        MHIP(hipEventRecord(m->g0[b], m->gather));
         for (uint32_t i = 0; i < n; ++i) {
             Shard &sh = m->s[i];
-            MHIP(hipStreamWaitEvent(m->gather, sh.traced[b], 0));
             const size_t bc = band_bytes(W, H, R, n, i, 4u);
             if (bc) MHIP(hipMemcpyPeerAsync(m->stage_cur + i * stride_cur, d0, sh.cur[b], sh.ordinal, bc, m->gather));
             if (bc && want_prev)
@@ -471,6 +535,7 @@ static int multi_trace(rt_multi *m, const rt_camera_info *cam, const rt_trace_de
          rtk_launch_assemble(m->stage_prev, stride_prev, cam->PreviousImage.Data, W, H, 16u, R, n, m->gather) != 0) ||
         rtk_launch_sum_u64(m->ray_slots, n, d_rays, m->gather) != 0)
         return rt_fail(RT_EIO, "rt_multi_trace: gather launch failed: %s", hipGetErrorString(hipGetLastError()));
+    MHIP(hipEventRecord(m->g1[b], m->gather));
     MHIP(hipEventRecord(m->gathered, m->gather));
     MHIP(hipStreamWaitEvent(caller, m->gathered, 0));
     m->last_band_rows = R;
@@ -500,6 +565,7 @@ extern "C" int rt_comm_unique_id(void *id_out) {
 }
 
 extern "C" int rt_comm_create(int hip_device, const void *id, uint32_t nranks, uint32_t rank, rt_comm **out) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!id || !out || nranks == 0 || rank >= nranks) return rt_fail(RT_EINVAL, "rt_comm_create: bad argument");
     *out = nullptr;
     if (!rccl().ok) return rt_fail(RT_ENODEV, "rt_comm_create: librccl.so.1 not loadable");
@@ -519,6 +585,7 @@ extern "C" int rt_comm_create(int hip_device, const void *id, uint32_t nranks, u
 }
 
 extern "C" int rt_comm_destroy(rt_comm *c) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c) return RT_OK;
     (void)hipSetDevice(c->ordinal);
     (void)hipDeviceSynchronize();
@@ -530,6 +597,7 @@ extern "C" int rt_comm_destroy(rt_comm *c) {
 
 extern "C" int rt_comm_gather_bands(rt_comm *c, const void *d_local, void *d_full, uint32_t width, uint32_t height,
                                     uint32_t elem_bytes, uint32_t band_rows, void *stream) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!c || width == 0 || height == 0 || elem_bytes == 0 || band_rows == 0 || band_rows % 8u)
         return rt_fail(RT_EINVAL, "rt_comm_gather_bands: bad argument");
     const uint32_t n = c->nranks;

@@ -209,3 +209,107 @@ def test_on_render_over_several_devices(rt, orc, torch_cuda):
         rt.on_render_wait()
     finally:
         rt.on_shutdown()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_back_to_back_continuations_gather_the_mean(rt, torch_cuda, devices):
+    """Continuations enqueued with no host synchronisation (PreviousRayCount 0,
+    S, 2S, 3S) that also gather the resident means: call k+1's traces overwrite
+    the means call k's gather reads, so they must wait for it (the
+    prev_gathered ordering on the copy / RCCL send events).  Each call's
+    gathered mean and frame equal one device's render of (k + 1) S frames.
+    [0] runs the RCCL transport (send/recv to itself), [0, 0, 0] peer copies."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 64)
+    W, H, S, B = 160, 96, 2, 8
+    cam = rt.camera_setup(s, W, H)
+    refs = [single(rt, torch, s, cam, W, H, (k + 1) * S, B) for k in range(4)]
+    m = rt.Multi(devices)
+    try:
+        m.upload_scene(s)
+        st = torch.cuda.current_stream().cuda_stream
+        outs = []
+        for k in range(4):
+            cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            prev = torch.full((W * H, 4), float("nan"), dtype=torch.float32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            m.trace(cam, width=W, height=H, cur_ptr=cur.data_ptr(), prev_ptr=prev.data_ptr(),
+                    rays_ptr=rays.data_ptr(), prev_count=k * S, frames=S, max_bounce=B, band_rows=8, stream=st)
+            outs.append((prev, cur, rays))
+        torch.cuda.synchronize()
+    finally:
+        m.close()
+    total = 0
+    for k, ((prev, cur, rays), ref) in enumerate(zip(outs, refs)):
+        total += int(rays.item())
+        assert total == ref[2], k
+        assert torch_equal_bits(prev, ref[0]), ("running mean differs", k)
+        assert torch_equal_bits(cur, ref[1]), ("RGBA8 differs", k)
+
+
+def test_multi_accum_zero_restart_at_a_nonzero_count_continues_from_there(rt, torch_cuda):
+    """RT_FLAG_ACCUM_ZERO with PreviousRayCount N > 0 folds its F frames with
+    the weights of N, N + 1, ... (like rt_trace), so the continuation names
+    N + F: N = 5, F = 2, then 3 more frames from 7; equal to one
+    device doing the same two launches."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 16)
+    W, H, B = 64, 48, 4
+    cam = rt.camera_setup(s, W, H)
+    dev = rt.Device(0)
+    try:
+        dev.upload_scene(s)
+        prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        for pc, f, az in ((5, 2, True), (7, 3, False)):
+            dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                      rays_ptr=rays.data_ptr(), prev_count=pc, frames=f, max_bounce=B, band_rows=8,
+                      accum_zero=az, stream=st)
+        torch.cuda.synchronize()
+    finally:
+        dev.close()
+    m = rt.Multi([0, 0])
+    try:
+        m.upload_scene(s)
+        multi_render(rt, torch, m, cam, W, H, 2, B, prev_count=5, accum_zero=True)
+        with pytest.raises(rt.RtError, match="holds 7 frames"):
+            multi_render(rt, torch, m, cam, W, H, 3, B, prev_count=2)
+        got = multi_render(rt, torch, m, cam, W, H, 3, B, prev_count=7)
+    finally:
+        m.close()
+    assert torch_equal_bits(got[0], prev) and torch_equal_bits(got[1], cur)
+
+
+def test_multi_reserve_means_no_allocation_in_later_calls(rt, orc, torch_cuda):
+    """rt_multi_reserve sizes every device's images, launch buffers and the
+    gather staging for a geometry: later calls of it (new cameras, P chosen per
+    launch by the frame count) grow nothing (BufferGrowths constant on every
+    device), report a gather time, and the slowest device's real launch info."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 64)
+    W, H, B = 200, 150, 8
+    m = rt.Multi([0, 0, 0])
+    try:
+        m.upload_scene(s)
+        m.reserve(W, H, 8, mean=True)
+        st = torch.cuda.current_stream().cuda_stream
+        cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        m.trace(rt.camera_setup(s, W, H), width=W, height=H, cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
+                frames=1, max_bounce=B, band_rows=8, accum_zero=True, stream=st)
+        torch.cuda.synchronize()
+        before = [m.shard_info(i)["BufferGrowths"] for i in range(3)]
+        for frames, dist in ((1, 5.0), (4, None), (32, 2.5), (3, None)):
+            cam = rt.camera_setup(s, W, H, distance=dist)
+            m.trace(cam, width=W, height=H, cur_ptr=cur.data_ptr(), prev_ptr=prev.data_ptr(),
+                    rays_ptr=rays.data_ptr(), frames=frames, max_bounce=B, band_rows=8, accum_zero=True, stream=st)
+        torch.cuda.synchronize()
+        after = [m.shard_info(i) for i in range(3)]
+        assert [a["BufferGrowths"] for a in after] == before
+        assert all(a["LanesPerPixel"] >= 1 for a in after)
+        assert m.last_gather_ms() >= 0.0
+    finally:
+        m.close()

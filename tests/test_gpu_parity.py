@@ -252,6 +252,35 @@ def test_on_render_busy_poll_hands_out_every_frame_in_order(rt, orc, torch_cuda)
         rt.on_shutdown()
 
 
+def test_on_render_fresh_image_every_call_and_registered_image(rt, orc, torch_cuda):
+    """A new host array on every call (freed buffers can come back at the same
+    address) gets every frame through the library's staging buffer: the
+    library page-locks nothing it was not handed.  A registered image gets the
+    same frames by DMA; after unregistering, the staged path serves it again."""
+    rt.on_init()
+    try:
+        W, H = 64, 40
+        o = orc.scene_builtin(0)
+        ocam = orc.camera(o, W, H)
+        rt.on_render(np.zeros((H, W), np.uint32), 0)
+        want = [orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5)[1] for k in range(6)]
+        for k in range(6):
+            if k == 2:
+                reg = np.zeros((H, W), np.uint32)
+                rt.on_render_register_image(reg)
+            if k == 4:
+                rt.on_render_unregister_image()
+            img = reg if k in (2, 3) else np.full((H, W), 0xDEADBEEF, np.uint32)
+            rt.on_render_wait()
+            done, _, _ = rt.on_render(img, 0)
+            assert done
+            assert np.array_equal(img.reshape(-1), want[k]), k
+            del img
+        rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
+
+
 def test_on_render_moving_camera_restarts_every_frame(rt, orc, torch_cuda):
     """RT_KEY_LEFT on every call (main.cpp:743-746): each call turns the camera
     by 1/16 rad, restarts the mean, and hands out the previous call's frame --
