@@ -1,15 +1,41 @@
-# A/B on one box: GPU parity under each env in $PARITY (';'-separated), then
-# bench C2 for each env config given as args (prints value, ms/step, kernel ms).
+# Same-box A/B of variants (the one A/B launcher; gpurun -- 'bash scripts/gpu_ab.sh').
+#   VARIANTS  ';'-separated; each is a list of env assignments, e.g.
+#             "RT_X=0;RT_SEC_THRESHOLD=24;RT_TRACE_LIB=librt_trace_base.so" (library builds:
+#             scripts/build_base_lib.sh, or make -C simd-ray-tracer_amd variant NAME=.. KFLAGS=..)
+#   CONFIGS   ';'-separated bench.py argument sets, "c2" = the defaults
+#             (default: "c2;--sim-ranks 8 --sim-index 3", the 8-rank share)
+#   ROUNDS    interleaved repetitions (default 3)
+#   PARITY=1  run the GPU suite under each variant first (stops at the first failure)
+#   STEPS / WARMUP  bench steps (default 10 / 6)
+# Prints one line per run: round, variant, config, Mrays/s, ms per step, kernel ms, cold ms.
 set -o pipefail
 mkdir -p gpurun_out
-IFS=';' read -ra PCFG <<< "${PARITY:-RT_LANES_PER_PIXEL=4}"
-i=0
-for cfg in "${PCFG[@]}"; do
-  i=$((i+1))
-  env $cfg timeout -k 10 600 python -m pytest tests -x -q -m gpu -p no:cacheprovider > gpurun_out/ab_pytest_$i.log 2>&1
-  rc=$?; echo "pytest [$cfg] rc=$rc $(tail -1 gpurun_out/ab_pytest_$i.log)"; [ $rc -ne 0 ] && { tail -30 gpurun_out/ab_pytest_$i.log; exit $rc; }
-done
-for cfg in "$@"; do
-  env $cfg timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/b.json 2> gpurun_out/b.err || { tail -20 gpurun_out/b.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('gpurun_out/b.json')); print('$cfg', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['config']['rays_per_step'], d.get('sched_stats',''))"
+IFS=';' read -ra VAR <<< "${VARIANTS:-RT_X=0}"
+IFS=';' read -ra CFG <<< "${CONFIGS:-c2;--sim-ranks 8 --sim-index 3}"
+ROUNDS=${ROUNDS:-3}
+if [ "${PARITY:-0}" = 1 ]; then
+  i=0
+  for v in "${VAR[@]}"; do
+    i=$((i+1))
+    env $v timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 200 \
+      --timeout-method thread > gpurun_out/ab_pytest_$i.log 2>&1
+    rc=$?; echo "parity [$v] rc=$rc $(tail -1 gpurun_out/ab_pytest_$i.log)"
+    [ $rc -ne 0 ] && { tail -30 gpurun_out/ab_pytest_$i.log; exit $rc; }
+  done
+fi
+for r in $(seq $ROUNDS); do
+  for v in "${VAR[@]}"; do
+    for c in "${CFG[@]}"; do
+      args=$c; [ "$c" = "c2" ] && args=""
+      env $v timeout -k 10 180 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-6} --no-cpu-baseline $args \
+        > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
+      python - "$r" "$v" "$c" <<'PY'
+import json, sys
+d = json.loads([l for l in open("gpurun_out/ab.json") if l.startswith("{")][-1])
+kern = d.get("roofline", {}).get("kernel_ms", d.get("rank0_kernel_ms"))
+print(sys.argv[1], f"[{sys.argv[2]}]", f"[{sys.argv[3]}]", d.get("value"), d.get("ms_per_step"), kern, "cold", d.get("cold_ms"),
+      flush=True)
+PY
+    done
+  done
 done
