@@ -243,6 +243,8 @@ typedef struct rt_trace_info {
                                  run-time dispatch, 1 per-group loops, 2/3/4
                                  cluster walk with 1/2/4 mask words, 5/6/7
                                  the same with per-lane thresholds           */
+    uint32_t PixelsPerLane;   /* 4: each lane traced 4 pixels in turn (one-lane-
+                                 per-pixel launches of one frame), else 1     */
     uint32_t BufferGrowths;   /* launch-buffer (re)allocations on this device
                                  so far (tile lists, cull masks): constant
                                  across launches that rt_device_reserve covers */

@@ -1,5 +1,7 @@
 """Diagnostic: per-wave start/end times of one C2 launch -> occupancy over time.
 env: SPP (256), SIM_RANKS (1: whole frame; G: rank 0's bands of a G-GPU split),
+SCENE (1) / SPHERES (64) / BOUNCES (8), CONTINUE (1: launches continue the running mean,
+as OnRender's frames do; default: every launch restarts it),
 RT_LANES_PER_PIXEL (auto), LAUNCHES (8: the learned order settles), SAVE (a .npz
 path: the raw per-wave {start, end} of the last launch, indexed 4 * block tile + wave,
 for offline schedule simulation: scripts/sched_sim.py)."""
@@ -12,8 +14,12 @@ os.environ["RT_WAVETIMES"] = "1"
 import torch
 import __graft_entry__ as graft
 rt = graft.load_package()
-W, H, S, B, N = 1920, 1080, int(os.environ.get("SPP", "256")), 8, 64
-scene = rt.scene_prefix(rt.scene_builtin(1), N)
+W, H, S = 1920, 1080, int(os.environ.get("SPP", "256"))
+B, N = int(os.environ.get("BOUNCES", "8")), int(os.environ.get("SPHERES", "64"))
+scene = rt.scene_builtin(int(os.environ.get("SCENE", "1")))
+if N < scene.ScalarSpheres.Count:
+    scene = rt.scene_prefix(scene, N)
+cont = os.environ.get("CONTINUE") == "1"
 cam = rt.camera_setup(scene, W, H)
 dev = rt.Device(0)
 dev.upload_scene(scene)
@@ -22,9 +28,10 @@ rows = rt.band_local_rows(H, 8, G, 0)
 prev = torch.zeros((rows * W, 4), dtype=torch.float32, device="cuda")
 cur = torch.zeros(rows * W, dtype=torch.int32, device="cuda")
 rays = torch.zeros(1, dtype=torch.int64, device="cuda")
-for _ in range(int(os.environ.get("LAUNCHES", "8"))):
+for i in range(int(os.environ.get("LAUNCHES", "8"))):
     dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(), rays_ptr=rays.data_ptr(),
-              frames=S, max_bounce=B, accum_zero=True, band_rows=8, band_count=G, band_index=0)
+              prev_count=i * S if cont else 0, frames=S, max_bounce=B, accum_zero=not cont, band_rows=8,
+              band_count=G, band_index=0)
 torch.cuda.synchronize()
 wt_all = dev.debug_wave_times().astype(np.int64)
 if os.environ.get("SAVE"):

@@ -51,6 +51,9 @@ struct rt_device {
     int wave_order_env = 1;     // RT_WAVE_ORDER=0: one-wave kernels order block tiles, not waves (A/B)
     int walk_any_env = 0;       // RT_WALK_ANY=1: the one-wave kernel dispatches the walk at run time (A/B)
     int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
+    // RT_PIXELS_PER_LANE: 0 auto (4 pixels per lane for one-lane-per-pixel launches of one
+    // frame), 1 never, 4 for every one-lane-per-pixel launch (A/B and the parity suite)
+    int pixels_per_lane_env = 0;
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
     int tile_sched = 1;
@@ -193,6 +196,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
         const int v = atoi(lp);
         d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
     }
+    const char *ppl = getenv("RT_PIXELS_PER_LANE");
+    if (ppl && (ppl[0] == '1' || ppl[0] == '4')) d->pixels_per_lane_env = ppl[0] - '0';
     const char *st = getenv("RT_STATS");
     if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatSlots * sizeof(unsigned long long)) == hipSuccess)
         (void)hipMemset(d->d_stats, 0, kStatSlots * sizeof(unsigned long long));
@@ -1062,11 +1067,22 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // (P=4 3.35); 4 ranks P=8 = P=16 1.81 ms; 8 ranks P=16 1.02 ms (P=8
     // 1.47)); never more lanes than frames.
     int lpp = d->lanes_per_pixel;
+    const bool auto_lpp = lpp == 0;
     if (lpp == 0) {
         const uint64_t pixels = (uint64_t)desc->Width * local_rows;
         lpp = pixels >= (uint64_t)d->cu_count * 6144u ? 4 : pixels >= (uint64_t)d->cu_count * 1536u ? 8 : 16;
         while (lpp > 1 && (uint32_t)lpp / 2u >= desc->Frames) lpp /= 2;
     }
+    // One lane per pixel, and one frame (the reference's OnRender unit): each lane
+    // takes kPixelsPerLane pixels in turn (launch shape 0, rt_kernel.hip Shape<0>),
+    // so a wave stays full after its first pass and the launch has a quarter of
+    // the waves.  Measured on the 1080p OnRender frame: see DESIGN.md §6a.
+    const uint32_t pixels_per_lane =
+        lpp == 1 && !(desc->Flags & RT_FLAG_SRGB_POW) &&
+                (d->pixels_per_lane_env == 4 || (d->pixels_per_lane_env == 0 && auto_lpp && desc->Frames == 1))
+            ? 4u : 1u;
+    const uint32_t lanes = (uint32_t)lpp;  // lanes per pixel (the sample chains of a pixel)
+    if (pixels_per_lane > 1) lpp = 0;      // the launch shape code of rtk_* (0: pixels per lane)
     // Tile scheduling.  Block tiles (2TW x 2TH pixels) are traced in the order
     // tile_order[0 .. n_live): with culling, the cull pass (once per camera /
     // scene / geometry) writes every wave tile's primary group mask and a
@@ -1170,11 +1186,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             // running mean heaviest-first.  Splitting a launch at a frame boundary
             // changes no bit: the owner lane folds frames in order either way, and
             // frame k's seed and weights depend on PreviousRayCount + k only.
-            const uint32_t split_min = 4u * d->head_samples * (uint32_t)lpp;
+            const uint32_t split_min = 4u * d->head_samples * lanes;
             if (sched && d->split_env && desc->Frames >= split_min) {
                 // leading parts of head_samples, x split_growth, ... samples per lane
                 // while the rest keeps at least half the frames
-                uint32_t f = d->head_samples * (uint32_t)lpp, used = 0;
+                uint32_t f = d->head_samples * lanes, used = 0;
                 for (uint32_t i = 0; i + 1 < d->split_parts && used + f <= desc->Frames / 2u; ++i) {
                     split[n_split++] = f;
                     used += f;
@@ -1203,7 +1219,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     d->last_n_tiles = n_tiles;
     d->last_frames = desc->Frames;
     d->last_empty_capable = empty_capable;
-    d->last.LanesPerPixel = (uint32_t)lpp;
+    d->last.LanesPerPixel = lanes;
+    d->last.PixelsPerLane = pixels_per_lane;
     d->last.TilesTotal = n_tiles;
     d->last.CullPassRan = cull && new_key ? 1u : 0u;
     d->last.OrderedLaunches = d->n_sorts;

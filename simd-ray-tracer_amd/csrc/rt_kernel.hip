@@ -50,16 +50,25 @@ __device__ __forceinline__ float rand_float(uint64_t &s, float lo, float inv) { 
     return r + lo;
 }
 
-__device__ __forceinline__ uint64_t seed_mix(uint64_t i) {  // main.cpp:668-675
-    uint64_t s = 0x420247153476526ULL * i;
-    s += 0x8442885C91A5C8DULL;
-    s ^= s >> ((7u + i) % 64u);
+// The seed mixer (main.cpp:668-675) from its first step's value u = C1 i + C2
+// and i's low 32 bits (the two shift counts need only i mod 64).  A lane's
+// consecutive samples k, k + P, ... have i = (k H + y) W + x a constant
+// P H W apart, so the kernel keeps u and i for the lane's next sample and steps
+// them with two adds instead of forming i and C1 i (64-bit multiplies, which
+// issue at half rate) per sample.
+constexpr uint64_t kSeedC1 = 0x420247153476526ULL, kSeedC2 = 0x8442885C91A5C8DULL;
+__device__ __forceinline__ uint64_t seed_finish(uint64_t s, uint32_t ilo) {
+    s ^= s >> ((7u + ilo) % 64u);
     s ^= s << 23;
-    s ^= s >> ((0x29u ^ i) % 64u);
+    s ^= s >> ((0x29u ^ ilo) % 64u);
     s = (s * 0x11C19226CEB4769AULL) + 0x1105404122082911ULL;
     s ^= s << 19;
     s ^= s >> 13;
     return s;
+}
+
+__device__ __forceinline__ uint64_t seed_mix(uint64_t i) {  // main.cpp:668-675
+    return seed_finish(kSeedC1 * i + kSeedC2, (uint32_t)i);
 }
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
@@ -222,8 +231,9 @@ __device__ __forceinline__ cargs_t &kernel_args() {
 }
 
 template <typename Args>
-__device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t y, uint32_t frame, Sample &p) {
-    p.rng = seed_mix(((uint64_t)frame * a.height + y) * a.width + x);
+__device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t y, uint64_t seed_u, uint32_t seed_i,
+                                             Sample &p) {
+    p.rng = seed_finish(seed_u, seed_i);  // seed_mix(((frame H) + y) W + x), frame = PreviousRayCount + k
     const float jx = rand_float(p.rng, -0.5f, kInvRange1);
     const float jy = rand_float(p.rng, -0.5f, kInvRange1);
     // ((x + Jx) * 2) / W with W's reciprocal RN(1/W) from the host: the
@@ -933,11 +943,20 @@ struct Ring {
 // splits the long per-pixel sample chains of pixels that see geometry over
 // several lanes: the heaviest waves get P times shorter, which removes most
 // of the kernel's tail.  Tiles: P=1 8x8, P=2 8x4, P=4 4x4 pixels per wave.
+// P = 0 is the other direction, for launches of one frame (the reference's
+// OnRender unit): one lane per pixel and kPixelsPerLane pixels per lane over a
+// 16x16 wave tile (slot q of lane l: the 8x8 quadrant q, pixel l of it).  A
+// lane whose path ends starts its next pixel's sample in the next primary
+// round, so a wave stays full instead of draining after one pass, and a
+// launch has a quarter of the waves (each of which pays the wave's setup once).
+constexpr uint32_t kPixelsPerLane = 4;
 template <int P>
 struct Shape {
-    static constexpr uint32_t TW = P <= 2 ? 8u : P <= 8 ? 4u : 2u;
-    static constexpr uint32_t TH = P == 1 ? 8u : P <= 4 ? 4u : P <= 16 ? 2u : 1u;
-    static_assert(TW * TH * P == 64, "a wave is 64 lanes");
+    static constexpr uint32_t LP = P == 0 ? 1u : (uint32_t)P;         // lanes per pixel
+    static constexpr uint32_t Q = P == 0 ? kPixelsPerLane : 1u;       // pixels per lane
+    static constexpr uint32_t TW = P == 0 ? 16u : P <= 2 ? 8u : P <= 8 ? 4u : 2u;
+    static constexpr uint32_t TH = P == 0 ? 16u : P == 1 ? 8u : P <= 4 ? 4u : P <= 16 ? 2u : 1u;
+    static_assert(TW * TH * LP == 64u * Q, "a wave is 64 lanes");
 };
 
 // GS: the scene (groups + materials) stays in HBM and per-lane gathers read it
@@ -978,8 +997,9 @@ void trace_kernel(TraceArgs a) {
     static_assert(!GS || SRC == kSrcSmem, "a scene in HBM is read through the scalar cache");
     static_assert(!SOLO || GS, "a one-wave workgroup keeps no LDS image");
     constexpr uint32_t kWB = SOLO ? 1u : (uint32_t)kWavesPerBlock;  // waves (LDS slots) per workgroup
-    constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, NPIX = 64u / P;
-    constexpr uint32_t kRing = Ring<P>::N;
+    constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, LP = Shape<P>::LP, Q = Shape<P>::Q;
+    constexpr uint32_t NPIX = 64u / LP;  // pixels traced at a time
+    constexpr uint32_t kRing = Ring<LP>::N;
     extern __shared__ float4 smem[];
     // first launch of a key: the host has not read the live-tile count back, so
     // the grid covers every tile (live first) and blocks past the count leave
@@ -995,7 +1015,7 @@ void trace_kernel(TraceArgs a) {
     // ring slot s of pixel pl at s * kRingStride + pl: the sample lanes of a
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
-    __shared__ float4 s_ring[P > 1 ? kWB * kRing * kRingStride : 1];
+    __shared__ float4 s_ring[LP > 1 ? kWB * kRing * kRingStride : 1];
     const uint32_t lut_f4 = a.lut_in_lds ? 512u : 0u;  // see rtk_lds_bytes
     const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, a.lut_in_lds != 0u};
     float2 *fold = reinterpret_cast<float2 *>(smem + lut_f4);
@@ -1041,15 +1061,29 @@ void trace_kernel(TraceArgs a) {
     }
     const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
     const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t pl = lane / P, j = lane % P;  // pixel of the tile, sample lane of the pixel
+    const uint32_t pl = lane / LP, j = lane % LP;  // pixel of the tile, sample lane of the pixel
     // wave tile: a TW x TH quadrant of the block tile, or (interleave) every
-    // other pixel and row of the whole block tile, parity (wave & 1, wave >> 1)
-    const uint32_t x = a.interleave ? tile_x * (2u * TW) + 2u * (pl % TW) + (wave & 1u)
-                                    : tile_x * (2u * TW) + (wave & 1u) * TW + pl % TW;
-    const uint32_t ly = a.interleave ? tile_y * (2u * TH) + 2u * (pl / TW) + (wave >> 1)
-                                     : tile_y * (2u * TH) + (wave >> 1) * TH + pl / TW;
-    const bool valid = x < a.width && ly < a.local_rows;
-    const uint32_t y = ((ly / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly % a.band_rows;
+    // other pixel and row of the whole block tile, parity (wave & 1, wave >> 1);
+    // Q > 1: pixel slot q of the lane is pixel pl of the tile's 8x8 quadrant q
+    auto pixel_x = [&](uint32_t q) -> uint32_t {
+        if (Q > 1) return tile_x * (2u * TW) + (wave & 1u) * TW + (pl & 7u) + 8u * (q & 1u);
+        return a.interleave ? tile_x * (2u * TW) + 2u * (pl % TW) + (wave & 1u)
+                            : tile_x * (2u * TW) + (wave & 1u) * TW + pl % TW;
+    };
+    auto pixel_ly = [&](uint32_t q) -> uint32_t {
+        if (Q > 1) return tile_y * (2u * TH) + (wave >> 1) * TH + (pl >> 3) + 8u * (q >> 1);
+        return a.interleave ? tile_y * (2u * TH) + 2u * (pl / TW) + (wave >> 1)
+                            : tile_y * (2u * TH) + (wave >> 1) * TH + pl / TW;
+    };
+    uint32_t q_slot = 0;  // Q > 1: the lane's current pixel slot
+    uint32_t x = pixel_x(0), ly = pixel_ly(0);
+    bool valid = x < a.width && ly < a.local_rows;
+    // (slot 0 outside the image puts every slot of the lane outside it: the
+    // slots lie right of and below slot 0)
+    auto global_y = [&](uint32_t l) -> uint32_t {
+        return ((l / a.band_rows) * a.band_count + a.band_index) * a.band_rows + l % a.band_rows;
+    };
+    uint32_t y = global_y(ly);
     const bool owner = j == 0;
     // The running mean of a pixel is one sequential chain per colour channel, so
     // with P >= 4 its lanes j = 0, 1, 2 each fold ONE channel (kept in accx) in
@@ -1057,13 +1091,13 @@ void trace_kernel(TraceArgs a) {
     // wave folds 3 chains per pixel at once (at P = 16 the owner's three-channel
     // fold was ~15 % of the wave's VALU instructions).  The owner gathers the
     // other two channels by DPP for the final store.
-    constexpr bool FOLD3 = P >= 4;
+    constexpr bool FOLD3 = LP >= 4;
     const bool folder = FOLD3 ? j < 3u : owner;
     // the channel a lane reads from a ring slot (lanes j >= 3 of the whole-batch fold
     // read the ratio word and discard their sums)
     const uint32_t jc = j < 3u ? j : 3u;
     // every lane of a pixel keeps the fold cursor (whole-batch frontier fold)
-    constexpr bool kCursorPerLane = P > 1;
+    constexpr bool kCursorPerLane = LP > 1;
     float4 *ring = s_ring + sw * kRing * kRingStride + pl;
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
@@ -1074,16 +1108,29 @@ void trace_kernel(TraceArgs a) {
     const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
 
     float accx = 0.0f, accy = 0.0f, accz = 0.0f;  // FOLD3: accx = this folding lane's channel j
-    if (valid && folder && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
-        const float4 pv = a.prev[(size_t)ly * a.width + x];
-        if (FOLD3) {
-            accx = j == 0u ? pv.x : j == 1u ? pv.y : pv.z;
-        } else {
-            accx = pv.x;
-            accy = pv.y;
-            accz = pv.z;
+    // the running mean so far of the lane's current pixel (main.cpp:485)
+    auto load_mean = [&]() {
+        accx = accy = accz = 0.0f;
+        if (valid && folder && a.prev_count > 0 && !(a.flags & kFlagAccumZero)) {
+            const float4 pv = a.prev[(size_t)ly * a.width + x];
+            if (FOLD3) {
+                accx = j == 0u ? pv.x : j == 1u ? pv.y : pv.z;
+            } else {
+                accx = pv.x;
+                accy = pv.y;
+                accz = pv.z;
+            }
         }
-    }
+    };
+    load_mean();
+    // the blended mean and its RGBA8 (main.cpp:488-492) of the current pixel
+    // (Q > 1 stores inside the trace loop, where the f64 pow of RT_FLAG_SRGB_POW
+    // would cost registers: the host launches that flag with Q = 1 only)
+    auto store_pixel = [&]() {
+        const size_t pix = (size_t)ly * a.width + x;
+        a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
+        a.cur[pix] = rgba8(accx, accy, accz, Q == 1 && (a.flags & kFlagSrgbPow) != 0u);
+    };
 
     // owner lanes of in-image pixels (they fold until every frame is folded)
     const uint64_t folding = ballot_and(owner, valid);
@@ -1091,6 +1138,17 @@ void trace_kernel(TraceArgs a) {
     uint32_t k = j;            // this lane's next (or current) sample
     uint32_t folded = 0;       // owner: samples folded so far
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
+    // the seed mixer's first step C1 i + C2 and i (mod 2^32) of sample k (seed_finish),
+    // stepped by LP frames = LP H W pixels per sample of the lane
+    uint64_t seed_u;
+    uint32_t seed_i;
+    auto seed_reset = [&]() {
+        const uint64_t i = ((uint64_t)(a.prev_count + k) * a.height + y) * a.width + x;
+        seed_u = kSeedC1 * i + kSeedC2;
+        seed_i = (uint32_t)i;
+    };
+    seed_reset();
+    const uint64_t seed_step = (uint64_t)LP * a.height * a.width;
     uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
     uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
@@ -1114,8 +1172,8 @@ void trace_kernel(TraceArgs a) {
     bool empty_tile = CULL && !a.use_sky && a.max_bounce != 0;
     if (CULL)
         for (uint32_t w = 0; w < n_words; ++w) empty_tile = empty_tile && s_maskw[w] == 0;
-    if (empty_tile) {
-        // (an all-zero running mean stays exactly zero: nothing to fold)
+    // (an all-zero running mean stays exactly zero: nothing to fold)
+    auto fold_zero_frames = [&]() {
         if (valid && folder && (accx != 0.0f || accy != 0.0f || accz != 0.0f)) {
             for (uint32_t q = 0; q < a.frames; ++q) {
                 float ratio;
@@ -1129,7 +1187,25 @@ void trace_kernel(TraceArgs a) {
                 accz = 0.0f + accz * ratio;
             }
         }
-        nrays = (uint64_t)__builtin_popcountll(__ballot(valid && owner)) * a.frames;
+    };
+    if (empty_tile) {
+        if (Q > 1) {  // every pixel slot of the lane, each stored here
+            for (uint32_t q = 0; q < Q; ++q) {
+                if (q > 0) {
+                    x = pixel_x(q);
+                    ly = pixel_ly(q);
+                    valid = x < a.width && ly < a.local_rows;
+                    load_mean();
+                }
+                fold_zero_frames();
+                nrays += (uint64_t)__builtin_popcountll(__ballot(valid)) * a.frames;
+                if (valid) store_pixel();
+            }
+            valid = false;  // (nothing left for the final store)
+        } else {
+            fold_zero_frames();
+            nrays = (uint64_t)__builtin_popcountll(__ballot(valid && owner)) * a.frames;
+        }
         folded = a.frames;
         mode = 2u;
     }
@@ -1161,9 +1237,9 @@ void trace_kernel(TraceArgs a) {
     // the pixel's owner lane's fold cursor (first of its P-lane slice) via DPP
     auto fold_cursor = [&]() -> uint32_t {
         return kCursorPerLane ? folded
-               : P == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
-               : P == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
-               : P > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
+               : LP == 4 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0x00, 0xf, 0xf, false)    // quad_perm 0,0,0,0
+               : LP == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)folded, 0xA0, 0xf, 0xf, false)  // quad_perm 0,0,2,2
+               : LP > 4 ? (uint32_t)__shfl((int)folded, (int)(lane - j), 64)
                         : folded;
     };
     // The pixel's parked frontier: every sample below it is in the ring.  A lane's
@@ -1174,16 +1250,16 @@ void trace_kernel(TraceArgs a) {
     auto parked_frontier = [&]() -> uint32_t {
         uint32_t f = k;
 #define RTK_DMIN(CTRL) f = min(f, (uint32_t)__builtin_amdgcn_update_dpp((int)f, (int)f, CTRL, 0xf, 0xf, false))
-        if (P >= 2) RTK_DMIN(0xB1);   // quad_perm 1,0,3,2 (lane ^ 1)
-        if (P >= 4) RTK_DMIN(0x4E);   // quad_perm 2,3,0,1 (lane ^ 2)
-        if (P >= 8) RTK_DMIN(0x141);  // row_half_mirror (the other quad of the 8)
-        if (P >= 16) RTK_DMIN(0x140); // row_mirror (the other half of the row)
+        if (LP >= 2) RTK_DMIN(0xB1);   // quad_perm 1,0,3,2 (lane ^ 1)
+        if (LP >= 4) RTK_DMIN(0x4E);   // quad_perm 2,3,0,1 (lane ^ 2)
+        if (LP >= 8) RTK_DMIN(0x141);  // row_half_mirror (the other quad of the 8)
+        if (LP >= 16) RTK_DMIN(0x140); // row_mirror (the other half of the row)
 #undef RTK_DMIN
-        if (P >= 32) f = min(f, (uint32_t)__shfl_xor((int)f, 16, 64));
+        if (LP >= 32) f = min(f, (uint32_t)__shfl_xor((int)f, 16, 64));
         return min(f, a.frames);
     };
     auto fold_ring = [&]() {
-        if (P == 1) return;
+        if (LP == 1) return;
         // ---- running-mean blend (main.cpp:484-489) of every parked sample, in
         // order: Final = Out*(1/n) + Prev*((n-1)/n), the first product done by the
         // sample's lane.  Slots [folded, F) are all parked: no per-slot flags, no
@@ -1244,11 +1320,13 @@ void trace_kernel(TraceArgs a) {
         // the pixel's owner lane (first of its P-lane quad slice) via DPP
         uint32_t folded_g = fold_cursor();
         // (lane masks from single compares: see ballot_and)
-        bool ring_ok = P == 1 || k < folded_g + kRing;
+        bool ring_ok = LP == 1 || k < folded_g + kRing;
         bool can_start = mode == 0u && ring_ok;
-        uint64_t pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
+        uint64_t pri = LP == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         const uint64_t sec = __builtin_amdgcn_ballot_w64(mode == 1u);
-        const uint64_t alive = __builtin_amdgcn_ballot_w64(mode != 2u) | (folding & __builtin_amdgcn_ballot_w64(folded < a.frames));
+        // (one lane per pixel folds each sample as it ends: nothing left to fold then)
+        const uint64_t alive = __builtin_amdgcn_ballot_w64(mode != 2u) |
+                               (LP > 1 ? folding & __builtin_amdgcn_ballot_w64(folded < a.frames) : 0ull);
         if (alive == 0) break;
         const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
         // Secondary segments run the full sphere loop; let them gather until
@@ -1263,9 +1341,9 @@ void trace_kernel(TraceArgs a) {
             fold_ring();
             if (kStats && a.stats) st_cyc_fold += __builtin_amdgcn_s_memtime() - st_f0;
             folded_g = fold_cursor();
-            ring_ok = P == 1 || k < folded_g + kRing;
+            ring_ok = LP == 1 || k < folded_g + kRing;
             can_start = mode == 0u && ring_ok;
-            pri = P == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
+            pri = LP == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         }
         if ((pri | sec) != 0) {
             if (kStats && a.stats) {
@@ -1292,7 +1370,7 @@ void trace_kernel(TraceArgs a) {
             const bool traces = mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
             if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
             if (traces) {
-                if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
+                if (!do_sec) start_sample(kernel_args(), x, y, seed_u, seed_i, p);
                 bool done;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
@@ -1398,7 +1476,7 @@ void trace_kernel(TraceArgs a) {
                     const float ox = a.max_bounce == 0 ? 0.0f : p.cx;
                     const float oy = a.max_bounce == 0 ? 0.0f : p.cy;
                     const float oz = a.max_bounce == 0 ? 0.0f : p.cz;
-                    if (P == 1) {
+                    if (LP == 1) {
                         // ---- running-mean blend (main.cpp:484-489), in order by construction
                         const float2 fw = k < fold_n ? fold[k] : fold_weights(a.prev_count + k);
                         const float inv = fw.x, ratio = fw.y;
@@ -1413,8 +1491,28 @@ void trace_kernel(TraceArgs a) {
                         if (__builtin_expect(k >= fold_n, 0)) w = fold_weights(a.prev_count + k);
                         ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
-                    k += P;
+                    k += LP;
+                    seed_u += kSeedC1 * seed_step;
+                    seed_i += (uint32_t)seed_step;
                     mode = k < a.frames ? 0u : 2u;
+                    if (Q > 1 && mode == 2u) {
+                        // the pixel is complete: store it and move to the lane's next pixel
+                        // slot inside the image (its samples start from k = 0)
+                        store_pixel();
+                        while (mode == 2u && q_slot + 1u < Q) {
+                            q_slot += 1u;
+                            x = pixel_x(q_slot);
+                            ly = pixel_ly(q_slot);
+                            if (x < a.width && ly < a.local_rows) {
+                                y = global_y(ly);
+                                k = 0;
+                                seed_reset();
+                                folded = 0;
+                                load_mean();
+                                mode = 0u;
+                            }
+                        }
+                    }
                 } else {
                     mode = 1u;
                 }
@@ -1431,11 +1529,7 @@ void trace_kernel(TraceArgs a) {
         accy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(accx), 0x55, 0xf, 0xf, false));
         accz = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(accx), 0xAA, 0xf, 0xf, false));
     }
-    if (valid && owner && a.frames > 0) {
-        const size_t pix = (size_t)ly * a.width + x;
-        a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
-        a.cur[pix] = rgba8(accx, accy, accz, (a.flags & kFlagSrgbPow) != 0u);
-    }
+    if (Q == 1 && valid && owner && a.frames > 0) store_pixel();  // (Q > 1: stored as each pixel completes)
 
     // ---- ray counter (RaysCastInThread, main.cpp:390): one atomic per wave
     if (lane == 0 && nrays) atomicAdd(a.rays, (unsigned long long)nrays);
@@ -1537,10 +1631,13 @@ __global__ __launch_bounds__(256) void cull_kernel(TraceArgs a, uint32_t *live, 
     const uint32_t x1 = x0 + (a.interleave ? 2u : 1u) * (TW - 1u), ly1 = ly0 + (a.interleave ? 2u : 1u) * (TH - 1u);
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
-    // band_rows % 8 == 0 keeps the wave tile's rows in one band (2TH <= 8 when interleaved: P >= 2)
+    // the image rows of the wave tile's first and last band-local rows: the band
+    // map is increasing, so every row of the tile lies between them (a tile of
+    // 16 rows may span two 8-row bands, whose rows between are other devices':
+    // the cone then covers them too, which only makes it wider)
     const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
-    const Cone c = tile_cone(a, (double)x0 - 0.501, (double)x1 + 0.501, (double)y0 - 0.501,
-                             (double)(y0 + (ly1 - ly0)) + 0.501);
+    const uint32_t y1 = ((ly1 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly1 % a.band_rows;
+    const Cone c = tile_cone(a, (double)x0 - 0.501, (double)x1 + 0.501, (double)y0 - 0.501, (double)y1 + 0.501);
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     bool any = false;
     for (uint32_t w = 0; w < n_words; ++w) {
@@ -1815,6 +1912,7 @@ extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lane
         case 8: bw = 2u * rtk::Shape<8>::TW; bh = 2u * rtk::Shape<8>::TH; break;
         case 4: bw = 2u * rtk::Shape<4>::TW; bh = 2u * rtk::Shape<4>::TH; break;
         case 2: bw = 2u * rtk::Shape<2>::TW; bh = 2u * rtk::Shape<2>::TH; break;
+        case 0: bw = 2u * rtk::Shape<0>::TW; bh = 2u * rtk::Shape<0>::TH; break;
         default: bw = 2u * rtk::Shape<1>::TW; bh = 2u * rtk::Shape<1>::TH; break;
     }
     return ((width + bw - 1u) / bw) * ((local_rows + bh - 1u) / bh);
@@ -1833,7 +1931,7 @@ static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n
                        stream, *a)
     if (a->solo) {  // one wave per workgroup, no LDS image (the host clears the *_in_lds flags)
         // one walk per kernel for the culled production shapes; others dispatch at run time
-        if constexpr (P == 4 || P == 8 || P == 16) {
+        if constexpr (P == 0 || P == 4 || P == 8 || P == 16) {
             if (cull) {
 #define RTK_WALKS(S)                                                          \
     switch (a->walk) {                                                        \
@@ -1907,6 +2005,7 @@ extern "C" int rtk_launch_trace_grid(const TraceArgs *a, int simd, int src, int 
         case 8: launch_p<8>(a, simd, src, cull, n_blocks, stream); break;
         case 4: launch_p<4>(a, simd, src, cull, n_blocks, stream); break;
         case 2: launch_p<2>(a, simd, src, cull, n_blocks, stream); break;
+        case 0: launch_p<0>(a, simd, src, cull, n_blocks, stream); break;
         default: launch_p<1>(a, simd, src, cull, n_blocks, stream); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -1925,6 +2024,7 @@ extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull,
         case 8: F<8>(__VA_ARGS__); break;                    \
         case 4: F<4>(__VA_ARGS__); break;                    \
         case 2: F<2>(__VA_ARGS__); break;                    \
+        case 0: F<0>(__VA_ARGS__); break;                    \
         default: F<1>(__VA_ARGS__); break;                   \
     }
 

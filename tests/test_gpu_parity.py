@@ -101,6 +101,36 @@ def test_progressive_split_equals_single_launch(rt, orc, torch_cuda, gdev):
     assert_same(pa, ca, ra, *r)
 
 
+@pytest.mark.parametrize("scene_idx,n,W,H,G", [(0, None, 203, 77, 1), (1, 64, 150, 70, 1), (2, None, 96, 88, 3),
+                                                (1, 64, 200, 150, 8)])
+def test_one_frame_launches_take_four_pixels_per_lane(rt, orc, torch_cuda, gdev, scene_idx, n, W, H, G):
+    """The OnRender unit: launches of ONE frame (PreviousRayCount 0, 1, 2, as
+    OnRender folds them) run one lane per pixel with 4 pixels per lane over
+    16x16 wave tiles (rt_trace_info.PixelsPerLane); ragged images leave some
+    lanes' later pixel slots outside the image, and 8-row bands of G devices
+    make a wave tile span two bands (its cull cone covers both).  The running
+    mean and RGBA8 of every frame equal the oracle's, bit for bit."""
+    torch = torch_cuda
+    s, o = _scenes(rt, orc, scene_idx, n)
+    cam = rt.camera_setup(s, W, H)
+    ocam = orc.camera(o, W, H)
+    band_rows = 8 if G > 1 else 32
+    for r in range(G):
+        local = rt.band_local_rows(H, band_rows, G, r)
+        prev = torch.zeros((local * W, 4), dtype=torch.float32, device="cuda")
+        rows = [y for y in range(H) if (y // band_rows) % G == r]
+        for k in range(3):
+            g = gpu_render(rt, torch, gdev, s, cam, W, H, frames=1, bounces=5, prev_count=k, prev=prev,
+                           band_rows=band_rows, band_count=G, band_index=r)
+            assert gdev.last_info()["PixelsPerLane"] == 4
+            op, oc, _ = orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5)
+            op = op.reshape(H, W, 4)[rows].reshape(-1, 4)
+            oc = oc.reshape(H, W)[rows].reshape(-1)
+            gp = g[0].cpu().numpy().reshape(-1, 4)
+            assert np.array_equal(gp.view(np.uint32), op.view(np.uint32)), (r, k)
+            assert np.array_equal(g[1].cpu().numpy().view(np.uint32), oc), (r, k)
+
+
 def test_accum_zero_flag_ignores_stale_buffer(rt, orc, torch_cuda, gdev):
     s, o = _scenes(rt, orc, 1, 16)
     W, H = 32, 32
@@ -318,7 +348,9 @@ VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0
                 # four-wave workgroups with the LDS image (the default is one wave per
                 # workgroup, each kernel compiled for one secondary walk)
                 {"RT_SOLO": "0"}, {"RT_SOLO": "0", "RT_CLUSTERS": "2"}, {"RT_WALK_ANY": "1"},
-                {"RT_WALK_ANY": "1", "RT_CLUSTERS": "2"}, {"RT_LANES_PER_PIXEL": "16", "RT_CLUSTERS": "2"}]
+                {"RT_WALK_ANY": "1", "RT_CLUSTERS": "2"}, {"RT_LANES_PER_PIXEL": "16", "RT_CLUSTERS": "2"},
+                # 4 pixels per lane at every frame count (the one-frame launch shape), and never
+                {"RT_LANES_PER_PIXEL": "1", "RT_PIXELS_PER_LANE": "4"}, {"RT_PIXELS_PER_LANE": "1"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
