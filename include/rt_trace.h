@@ -245,6 +245,9 @@ typedef struct rt_trace_info {
                                  the same with per-lane thresholds           */
     uint32_t PixelsPerLane;   /* 4: each lane traced 4 pixels in turn (one-lane-
                                  per-pixel launches of one frame), else 1     */
+    uint32_t PixelsSorted;    /* 1: the block tiles' pixels were dealt to their
+                                 waves by the previous launch's costs
+                                 (RT_PIXEL_SORT=1)                           */
     uint32_t BufferGrowths;   /* launch-buffer (re)allocations on this device
                                  so far (tile lists, cull masks): constant
                                  across launches that rt_device_reserve covers */

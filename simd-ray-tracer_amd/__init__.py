@@ -91,7 +91,7 @@ class RtTraceDesc(ctypes.Structure):
 class RtTraceInfo(ctypes.Structure):  # rt_trace_last_info
     _fields_ = [("SegmentsFolded", c_uint64)] + [(n, c_uint32) for n in (
         "LanesPerPixel", "TilesTotal", "TilesTraced", "CullPassRan", "OrderedLaunches", "ClusteredWalk",
-        "GroupsPerRuleSet", "SplitHeadFrames", "OneWaveGroups", "Walk", "PixelsPerLane", "BufferGrowths")]
+        "GroupsPerRuleSet", "SplitHeadFrames", "OneWaveGroups", "Walk", "PixelsPerLane", "PixelsSorted", "BufferGrowths")]
 
 
 class RtMultiInfo(ctypes.Structure):  # rt_multi_get_info

@@ -54,6 +54,12 @@ struct rt_device {
     // RT_PIXELS_PER_LANE: 0 auto (4 pixels per lane for one-lane-per-pixel launches of one
     // frame), 1 never, 4 for every one-lane-per-pixel launch (A/B and the parity suite)
     int pixels_per_lane_env = 0;
+    // RT_PIXEL_SORT=1: each block tile's pixels dealt to its waves by the cost the
+    // last launch measured (rtk_launch_pixel_sort), at P >= 4
+    int pixel_sort_env = 0;
+    uint8_t *d_pix_perm = nullptr;  // 64 B per block tile (TraceArgs.pix_perm)
+    uint32_t *d_pix_cost = nullptr; // per band pixel (TraceArgs.pix_cost)
+    size_t pix_perm_cap = 0, pix_cost_cap = 0;
     // heaviest-first tile order learned from the previous launch of the same
     // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
     int tile_sched = 1;
@@ -196,6 +202,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
         const int v = atoi(lp);
         d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
     }
+    const char *psort = getenv("RT_PIXEL_SORT");
+    if (psort && psort[0] == '1') d->pixel_sort_env = 1;
     const char *ppl = getenv("RT_PIXELS_PER_LANE");
     if (ppl && (ppl[0] == '1' || ppl[0] == '4')) d->pixels_per_lane_env = ppl[0] - '0';
     const char *st = getenv("RT_STATS");
@@ -225,6 +233,8 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_tile_live);
     (void)hipFree(d->d_cull_counters);
     (void)hipFree(d->d_masks);
+    (void)hipFree(d->d_pix_perm);
+    (void)hipFree(d->d_pix_cost);
     if (d->h_counts) (void)hipHostFree(d->h_counts);
     if (d->ev_counts) (void)hipEventDestroy(d->ev_counts);
     if (d->stream) (void)hipStreamDestroy(d->stream);
@@ -958,6 +968,29 @@ static int ensure_masks(rt_device *d, size_t mask_words, hipStream_t sync, bool 
     return RT_OK;
 }
 
+static int ensure_pixel_sort(rt_device *d, uint32_t n_tiles, size_t pixels, hipStream_t sync, bool device_wide) {
+    if ((size_t)n_tiles * 64u <= d->pix_perm_cap && pixels * 4u <= d->pix_cost_cap) return RT_OK;
+    if (device_wide) HIP_OK(hipDeviceSynchronize());
+    else HIP_OK(hipStreamSynchronize(sync));
+    if ((size_t)n_tiles * 64u > d->pix_perm_cap) {
+        (void)hipFree(d->d_pix_perm);
+        d->d_pix_perm = nullptr;
+        d->pix_perm_cap = 0;
+        if (hipMalloc(&d->d_pix_perm, (size_t)n_tiles * 64u) != hipSuccess) return fail(RT_ENOMEM, "rt_trace: pixel order");
+        d->pix_perm_cap = (size_t)n_tiles * 64u;
+    }
+    if (pixels * 4u > d->pix_cost_cap) {
+        (void)hipFree(d->d_pix_cost);
+        d->d_pix_cost = nullptr;
+        d->pix_cost_cap = 0;
+        if (hipMalloc(&d->d_pix_cost, pixels * 4u) != hipSuccess) return fail(RT_ENOMEM, "rt_trace: pixel costs");
+        d->pix_cost_cap = pixels * 4u;
+    }
+    d->last.BufferGrowths += 1;
+    d->tile_key.clear();
+    return RT_OK;
+}
+
 // The buffers of every launch rt_trace may make at the reserved geometry:
 // the most block tiles over every lanes-per-pixel shape (rt_trace picks P per
 // launch) and the current scene's mask words, so no later launch allocates.
@@ -970,6 +1003,9 @@ static int apply_reserve(rt_device *d) {
     if (d->scene_set)
         for (int rs = 0; rs < 2; ++rs) n_words = std::max(n_words, (d->n_groups[rs] + 63u) / 64u);
     if (const int rc = ensure_tile_buffers(d, n_tiles, nullptr, true)) return rc;
+    if (d->pixel_sort_env)
+        if (const int rc = ensure_pixel_sort(d, n_tiles, (size_t)d->reserve_width * d->reserve_rows, nullptr, true))
+            return rc;
     return ensure_masks(d, (size_t)n_tiles * 4u * n_words, nullptr, true);
 }
 
@@ -1159,12 +1195,17 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     const size_t mask_words = (size_t)n_tiles * 4u * n_words;
     if (cull)
         if (const int rc = ensure_masks(d, mask_words, s, false)) return rc;
+    // pixels dealt to waves by cost (RT_PIXEL_SORT): block tiles of at most 64 pixels
+    const bool pixel_sort = d->pixel_sort_env && sched && lpp >= 4 && !a.interleave;
+    if (pixel_sort)
+        if (const int rc = ensure_pixel_sort(d, n_tiles, (size_t)desc->Width * local_rows, s, false)) return rc;
     const bool new_key = key != d->tile_key;
     uint32_t head_frames = 0;  // > 0: split this launch (first launch of a key, below): frames of the leading parts
     uint32_t split[8], n_split = 0;
     if (new_key) {
         d->tile_key = key;
         d->n_sorts = 0;
+        if (pixel_sort) HIP_OK(hipMemsetAsync(d->d_pix_perm, 0xFF, (size_t)n_tiles * 64u, s));  // identity
         if (cull) {
             a.masks = d->d_masks;
             d->mask_words = mask_words;
@@ -1216,6 +1257,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.masks = cull ? d->d_masks : nullptr;
     a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
     a.tile_cost = sched ? d->d_tile_cost : nullptr;
+    a.pix_perm = pixel_sort ? d->d_pix_perm : nullptr;
+    d->last.PixelsSorted = pixel_sort && !new_key && d->n_sorts > 0 ? 1u : 0u;
     d->last_n_tiles = n_tiles;
     d->last_frames = desc->Frames;
     d->last_empty_capable = empty_capable;
@@ -1240,6 +1283,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         }
         a.frames = split[part];
         done_frames += split[part];
+        const bool resort = sched && any_live && (d->n_sorts < d->order_launches || part + 1 < n_split);
+        a.pix_cost = pixel_sort && resort ? d->d_pix_cost : nullptr;
         if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, grid_tiles, s) != 0)
             return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         if (any_dead && rtk_launch_empty(&a, lpp, d->d_tile_live, d->d_cull_counters + kCullTotals + 1, s) != 0)
@@ -1248,10 +1293,12 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         // 5.8 ms); after order_launches re-sorts (RT_ORDER_LAUNCHES, default 6)
         // the order is kept and the three sort kernels (~14 us per launch, 1.5 %
         // of an 8-rank C2 share) are skipped
-        if (sched && any_live && (d->n_sorts < d->order_launches || part + 1 < n_split)) {
+        if (resort) {
             d->n_sorts += 1;
             if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_units, s) != 0)
                 return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
+            if (pixel_sort && rtk_launch_pixel_sort(&a, lpp, d->d_pix_perm, s) != 0)
+                return fail(RT_EIO, "rt_trace: pixel sort launch failed: %s", hipGetErrorString(hipGetLastError()));
             d->tile_order_valid = true;
         }
     }

@@ -84,6 +84,13 @@ struct TraceArgs {
     // one-wave kernels (solo): tile_order / tile_cost index WAVES (4 * block tile + quadrant),
     // so the heaviest-first order ranks every wave on its own cost (rt_host.cpp unit_waves)
     uint32_t unit_waves;
+    // optional (RT_PIXEL_SORT): the block tile's pixels dealt to its four waves by cost,
+    // cheapest first: pix_perm[64 * tile + NPIX * wave + pl] = the pixel's index in the
+    // block tile (row-major, 2TW wide); pix_perm[64 * tile] == 0xFF: not permuted
+    const uint8_t *pix_perm;
+    // optional: segments each pixel traced in this launch (band-local rows x width), the
+    // cost the next launch's permutation sorts by (rtk_launch_pixel_sort)
+    uint32_t *pix_cost;
 };
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)
 // striped image pixels of dead block tiles, then the two totals at kCullTotals
@@ -149,6 +156,12 @@ extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t
 // the cull pass's device total, so the host need not read it back).
 extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
                                 const unsigned long long *dead_pixels, hipStream_t stream);
+// Per block tile, deal its pixels to its four waves by the costs the last launch
+// measured (TraceArgs.pix_cost), cheapest to wave 0, so each wave's pixels finish
+// their samples at about the same time; blocks with a quadrant the cull pass
+// left empty keep their pixels (that quadrant's wave folds without tracing).
+// perm: 64 bytes per block tile (TraceArgs.pix_perm).  P in {4, 8, 16, 32}.
+extern "C" int rtk_launch_pixel_sort(const TraceArgs *a, int lanes_per_pixel, uint8_t *perm, hipStream_t stream);
 // dst[0] += sum of slots[0, n) (the gathered per-device ray counters)
 extern "C" int rtk_launch_sum_u64(const uint64_t *slots, uint32_t n, uint64_t *dst, hipStream_t stream);
 // Restores the caller's current HIP device when a C-ABI entry point returns:

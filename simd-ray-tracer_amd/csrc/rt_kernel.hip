@@ -50,25 +50,16 @@ __device__ __forceinline__ float rand_float(uint64_t &s, float lo, float inv) { 
     return r + lo;
 }
 
-// The seed mixer (main.cpp:668-675) from its first step's value u = C1 i + C2
-// and i's low 32 bits (the two shift counts need only i mod 64).  A lane's
-// consecutive samples k, k + P, ... have i = (k H + y) W + x a constant
-// P H W apart, so the kernel keeps u and i for the lane's next sample and steps
-// them with two adds instead of forming i and C1 i (64-bit multiplies, which
-// issue at half rate) per sample.
-constexpr uint64_t kSeedC1 = 0x420247153476526ULL, kSeedC2 = 0x8442885C91A5C8DULL;
-__device__ __forceinline__ uint64_t seed_finish(uint64_t s, uint32_t ilo) {
-    s ^= s >> ((7u + ilo) % 64u);
+__device__ __forceinline__ uint64_t seed_mix(uint64_t i) {  // main.cpp:668-675
+    uint64_t s = 0x420247153476526ULL * i;
+    s += 0x8442885C91A5C8DULL;
+    s ^= s >> ((7u + i) % 64u);
     s ^= s << 23;
-    s ^= s >> ((0x29u ^ ilo) % 64u);
+    s ^= s >> ((0x29u ^ i) % 64u);
     s = (s * 0x11C19226CEB4769AULL) + 0x1105404122082911ULL;
     s ^= s << 19;
     s ^= s >> 13;
     return s;
-}
-
-__device__ __forceinline__ uint64_t seed_mix(uint64_t i) {  // main.cpp:668-675
-    return seed_finish(kSeedC1 * i + kSeedC2, (uint32_t)i);
 }
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
@@ -231,9 +222,8 @@ __device__ __forceinline__ cargs_t &kernel_args() {
 }
 
 template <typename Args>
-__device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t y, uint64_t seed_u, uint32_t seed_i,
-                                             Sample &p) {
-    p.rng = seed_finish(seed_u, seed_i);  // seed_mix(((frame H) + y) W + x), frame = PreviousRayCount + k
+__device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t y, uint32_t frame, Sample &p) {
+    p.rng = seed_mix(((uint64_t)frame * a.height + y) * a.width + x);
     const float jx = rand_float(p.rng, -0.5f, kInvRange1);
     const float jy = rand_float(p.rng, -0.5f, kInvRange1);
     // ((x + Jx) * 2) / W with W's reciprocal RN(1/W) from the host: the
@@ -1084,6 +1074,16 @@ void trace_kernel(TraceArgs a) {
         return ((l / a.band_rows) * a.band_count + a.band_index) * a.band_rows + l % a.band_rows;
     };
     uint32_t y = global_y(ly);
+    // pixels dealt to the block's waves by cost (rtk_launch_pixel_sort): wave-uniform
+    const uint8_t *perm = Q == 1 && a.pix_perm && !a.interleave ? a.pix_perm + (size_t)tile * 64u : nullptr;
+    const bool permuted = perm && perm[0] != 0xFFu;
+    if (permuted) {
+        const uint32_t li = perm[wave * NPIX + pl];
+        x = tile_x * (2u * TW) + li % (2u * TW);
+        ly = tile_y * (2u * TH) + li / (2u * TW);
+        valid = x < a.width && ly < a.local_rows;
+        y = global_y(ly);
+    }
     const bool owner = j == 0;
     // The running mean of a pixel is one sequential chain per colour channel, so
     // with P >= 4 its lanes j = 0, 1, 2 each fold ONE channel (kept in accx) in
@@ -1102,7 +1102,13 @@ void trace_kernel(TraceArgs a) {
 
     const uint32_t n_words = (a.n_groups + 63u) / 64u;
     // the wave tile's primary group mask, from the cull pass (rtk_launch_cull)
-    if (CULL && lane < n_words) s_maskw[lane] = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
+    // (a permuted wave's pixels come from all four quadrants: the union of their masks)
+    if (CULL && lane < n_words) {
+        uint64_t m = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
+        if (permuted)
+            for (uint32_t q = 0; q < 4u; ++q) m |= a.masks[((size_t)tile * 4u + q) * n_words + lane];
+        s_maskw[lane] = m;
+    }
     const uint64_t st_c1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
@@ -1138,18 +1144,9 @@ void trace_kernel(TraceArgs a) {
     uint32_t k = j;            // this lane's next (or current) sample
     uint32_t folded = 0;       // owner: samples folded so far
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
-    // the seed mixer's first step C1 i + C2 and i (mod 2^32) of sample k (seed_finish),
-    // stepped by LP frames = LP H W pixels per sample of the lane
-    uint64_t seed_u;
-    uint32_t seed_i;
-    auto seed_reset = [&]() {
-        const uint64_t i = ((uint64_t)(a.prev_count + k) * a.height + y) * a.width + x;
-        seed_u = kSeedC1 * i + kSeedC2;
-        seed_i = (uint32_t)i;
-    };
-    seed_reset();
-    const uint64_t seed_step = (uint64_t)LP * a.height * a.width;
+
     uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
+    uint32_t pseg = 0;   // segments this lane traced (pix_cost)
     uint32_t st_pri_it = 0, st_pri_lanes = 0, st_sec_it = 0, st_sec_lanes = 0, st_groups = 0, st_sec_hit = 0;
     uint32_t st_sparse_it = 0, st_sparse_lanes = 0, st_tail_it = 0;
     uint32_t st_pri_blocked = 0, st_pri_waitsec = 0, st_pri_done = 0;
@@ -1370,7 +1367,8 @@ void trace_kernel(TraceArgs a) {
             const bool traces = mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
             if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
             if (traces) {
-                if (!do_sec) start_sample(kernel_args(), x, y, seed_u, seed_i, p);
+                pseg += 1u;
+                if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
                 bool done;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
@@ -1492,8 +1490,6 @@ void trace_kernel(TraceArgs a) {
                         ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
                     k += LP;
-                    seed_u += kSeedC1 * seed_step;
-                    seed_i += (uint32_t)seed_step;
                     mode = k < a.frames ? 0u : 2u;
                     if (Q > 1 && mode == 2u) {
                         // the pixel is complete: store it and move to the lane's next pixel
@@ -1506,7 +1502,6 @@ void trace_kernel(TraceArgs a) {
                             if (x < a.width && ly < a.local_rows) {
                                 y = global_y(ly);
                                 k = 0;
-                                seed_reset();
                                 folded = 0;
                                 load_mean();
                                 mode = 0u;
@@ -1531,6 +1526,10 @@ void trace_kernel(TraceArgs a) {
     }
     if (Q == 1 && valid && owner && a.frames > 0) store_pixel();  // (Q > 1: stored as each pixel completes)
 
+    if (a.pix_cost) {  // the pixel's traced segments over its P lanes (every lane active here)
+        for (uint32_t off = 1; off < LP; off <<= 1) pseg += (uint32_t)__shfl_xor((int)pseg, (int)off, 64);
+        if (Q == 1 && valid && owner) a.pix_cost[(size_t)ly * a.width + x] = pseg;
+    }
     // ---- ray counter (RaysCastInThread, main.cpp:390): one atomic per wave
     if (lane == 0 && nrays) atomicAdd(a.rays, (unsigned long long)nrays);
     if (a.tile_cost && lane == 0) {
@@ -1738,6 +1737,38 @@ __global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t 
 }
 
 #ifndef RTK_P16_TU  // (the P = 16 translation unit holds only its trace launches: see launch_p16)
+// One wave per block tile: rank its pixels by the last launch's cost (ties by
+// index), so wave w of the next launch gets ranks [NPIX w, NPIX (w + 1)).
+template <int P>
+__global__ __launch_bounds__(64) void pixel_sort_kernel(TraceArgs a, uint8_t *perm) {
+    constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, BW = 2u * TW, NB = 4u * TW * TH;
+    static_assert(NB <= 64, "a block tile's pixels fit one wave");
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
+    uint8_t *pp = perm + (size_t)tile * 64u;
+    // a quadrant without candidate groups folds without tracing: keep such blocks as they are
+    if (a.masks) {
+        const uint32_t n_words = (a.n_groups + 63u) / 64u;
+        bool live = false;
+        for (uint32_t w = 0; lane < 4u && w < n_words; ++w) live = live || a.masks[((size_t)tile * 4u + lane) * n_words + w] != 0;
+        if (__builtin_popcountll(__ballot(lane < 4u && live)) != 4) {
+            if (lane == 0) pp[0] = 0xFFu;
+            return;
+        }
+    }
+    uint32_t c = 0;
+    if (lane < NB) {
+        const uint32_t x = tile_x * BW + lane % BW, ly = tile_y * (2u * TH) + lane / BW;
+        c = x < a.width && ly < a.local_rows ? a.pix_cost[(size_t)ly * a.width + x] : 0u;
+    }
+    uint32_t rank = 0;
+    for (uint32_t i = 0; i < NB; ++i) {
+        const uint32_t ci = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)i);
+        rank += ci < c || (ci == c && i < lane) ? 1u : 0u;
+    }
+    if (lane < NB) pp[rank] = (uint8_t)lane;
+}
+
 // Scatter RCCL-gathered compact band images into the full framebuffer.
 __global__ __launch_bounds__(256) void assemble_kernel(const uint8_t *src, uint64_t rank_stride, uint8_t *dst,
                                                        uint32_t width, uint32_t height, uint32_t elem,
@@ -2055,6 +2086,23 @@ static void launch_empty_p(const TraceArgs *a, const uint32_t *live, const unsig
 extern "C" int rtk_launch_empty(const TraceArgs *a, int lanes_per_pixel, const uint32_t *live,
                                 const unsigned long long *dead_pixels, hipStream_t stream) {
     RTK_BY_P(launch_empty_p, a, live, dead_pixels, stream)
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+template <int P>
+static void launch_pixel_sort_p(const TraceArgs *a, uint8_t *perm, hipStream_t stream) {
+    const uint32_t n = rtk_tile_count(a->width, a->local_rows, P);
+    hipLaunchKernelGGL(rtk::pixel_sort_kernel<P>, dim3(n), dim3(64), 0, stream, *a, perm);
+}
+
+extern "C" int rtk_launch_pixel_sort(const TraceArgs *a, int lanes_per_pixel, uint8_t *perm, hipStream_t stream) {
+    switch (a->pix_cost ? lanes_per_pixel : 0) {  // (a block tile of 64 pixels at most: P >= 4)
+        case 32: launch_pixel_sort_p<32>(a, perm, stream); break;
+        case 16: launch_pixel_sort_p<16>(a, perm, stream); break;
+        case 8: launch_pixel_sort_p<8>(a, perm, stream); break;
+        case 4: launch_pixel_sort_p<4>(a, perm, stream); break;
+        default: return -1;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 #undef RTK_BY_P

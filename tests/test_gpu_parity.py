@@ -131,6 +131,38 @@ def test_one_frame_launches_take_four_pixels_per_lane(rt, orc, torch_cuda, gdev,
             assert np.array_equal(g[1].cpu().numpy().view(np.uint32), oc), (r, k)
 
 
+@pytest.mark.parametrize("scene_idx,n,W,H,spp,B,lpp", [(1, 64, 96, 80, 8, 8, "4"), (2, None, 72, 56, 8, 5, "4"),
+                                                       (0, None, 64, 48, 16, 5, "8"), (1, 200, 40, 32, 16, 8, "16")])
+def test_pixels_dealt_by_cost_keep_every_bit(rt, orc, torch_cuda, monkeypatch, scene_idx, n, W, H, spp, B, lpp):
+    """RT_PIXEL_SORT=1: after a launch measures each pixel's traced segments,
+    every block tile's pixels are dealt to its four waves cheapest first (and
+    a permuted wave tests the union of the block's quadrant masks).  Repeated
+    launches with the permutation in place equal the oracle bit for bit."""
+    monkeypatch.setenv("RT_PIXEL_SORT", "1")
+    monkeypatch.setenv("RT_LANES_PER_PIXEL", lpp)
+    dev = rt.Device(0)
+    try:
+        s, o = _scenes(rt, orc, scene_idx, n)
+        cam = rt.camera_setup(s, W, H)
+        r = orc.render(o, orc.camera(o, W, H), W, H, frames=spp, max_bounce=B)
+        dev.upload_scene(s)
+        torch = torch_cuda
+        sorted_launches = 0
+        for _ in range(4):
+            prev = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            cur = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            rays = torch.zeros(1, dtype=torch.int64, device="cuda")
+            dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                      rays_ptr=rays.data_ptr(), frames=spp, max_bounce=B, accum_zero=True,
+                      stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert_same(prev, cur, int(rays.item()), *r)
+            sorted_launches += dev.last_info()["PixelsSorted"]
+        assert sorted_launches == 3
+    finally:
+        dev.close()
+
+
 def test_accum_zero_flag_ignores_stale_buffer(rt, orc, torch_cuda, gdev):
     s, o = _scenes(rt, orc, 1, 16)
     W, H = 32, 32
