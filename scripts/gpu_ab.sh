@@ -35,6 +35,8 @@ d = json.loads([l for l in open("gpurun_out/ab.json") if l.startswith("{")][-1])
 kern = d.get("roofline", {}).get("kernel_ms", d.get("rank0_kernel_ms"))
 print(sys.argv[1], f"[{sys.argv[2]}]", f"[{sys.argv[3]}]", d.get("value"), d.get("ms_per_step"), kern, "cold", d.get("cold_ms"),
       flush=True)
+for r in d.get("runs", [])[1:]:  # (onrender: the other sizes / modes)
+    print("   ", r["width"], r["mode"], r["mrays_per_s"], r["ms_per_frame"], "gpu", r.get("gpu_ms_per_frame"), flush=True)
 PY
     done
   done

@@ -57,6 +57,7 @@ struct rt_device {
     // RT_PIXEL_SORT=1: each block tile's pixels dealt to its waves by the cost the
     // last launch measured (rtk_launch_pixel_sort), at P >= 4
     int pixel_sort_env = 0;
+    int merge_env = -1;  // RT_MERGE_ROUNDS: -1 auto (scenes of at most kMergeGroups groups), 0 never, 1 always
     uint8_t *d_pix_perm = nullptr;  // 64 B per block tile (TraceArgs.pix_perm)
     uint32_t *d_pix_cost = nullptr; // per band pixel (TraceArgs.pix_cost)
     size_t pix_perm_cap = 0, pix_cost_cap = 0;
@@ -202,6 +203,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
         const int v = atoi(lp);
         d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
     }
+    const char *mr = getenv("RT_MERGE_ROUNDS");
+    if (mr && (mr[0] == '0' || mr[0] == '1')) d->merge_env = mr[0] - '0';
     const char *psort = getenv("RT_PIXEL_SORT");
     if (psort && psort[0] == '1') d->pixel_sort_env = 1;
     const char *ppl = getenv("RT_PIXELS_PER_LANE");
@@ -1090,6 +1093,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // pays to fill it first.  Measured (same box, Mrays/s, threshold 16/32/40/48):
     // RTWeekend (20 cluster pairs) 18.6k/19.4k/19.5k/19.5k, C5 at 512 spp (16)
     // 44.7k/46.3k/46.4k/46.4k, C2 (5) 153.8k/151.2k/150.4k/149.9k.
+    a.merge_rounds = d->merge_env == 1 || (d->merge_env == -1 && d->n_groups[rs] <= kMergeGroups) ? 1u : 0u;
     a.sec_threshold = d->sec_threshold;
     if (a.sec_threshold == 0) a.sec_threshold = (a.clusters ? a.n_cpairs : a.n_groups) >= 12u ? 40u : 16u;
     a.stats = d->d_stats;

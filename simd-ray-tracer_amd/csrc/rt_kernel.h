@@ -91,7 +91,12 @@ struct TraceArgs {
     // optional: segments each pixel traced in this launch (band-local rows x width), the
     // cost the next launch's permutation sorts by (rtk_launch_pixel_sort)
     uint32_t *pix_cost;
+    // 1: every round starts new samples and continues paths together through the exact
+    // sphere loop (scenes of at most kMergeGroups groups: the cull mask and the prefilter
+    // save nothing there, and split rounds leave most lanes idle at one frame per launch)
+    uint32_t merge_rounds;
 };
+constexpr uint32_t kMergeGroups = 2;
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)
 // striped image pixels of dead block tiles, then the two totals at kCullTotals
 // (live tiles, dead pixels), summed on the device after the pass.

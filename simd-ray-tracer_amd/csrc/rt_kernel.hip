@@ -976,6 +976,8 @@ struct Shape {
 constexpr int solo_waves(int walk) { return walk == kWalkCl2 ? RTK_SOLO_WAVES_CL2 : RTK_SOLO_WAVES_PER_SIMD; }
 
 template <int WALK> struct Walk {
+    // the per-group walk (small scenes) may merge primary and secondary rounds
+    static constexpr bool MERGEABLE = WALK == kWalkAny || WALK == kWalkGroups;
     static constexpr int W = WALK == kWalkCl2 || WALK == kWalkCl2Rel ? 2 : WALK == kWalkCl4 || WALK == kWalkCl4Rel ? 4 : 1;
     static constexpr bool REL = WALK == kWalkCl1Rel || WALK == kWalkCl2Rel || WALK == kWalkCl4Rel;
     static constexpr bool CLUSTERS = WALK >= kWalkCl1;
@@ -989,6 +991,7 @@ void trace_kernel(TraceArgs a) {
     constexpr uint32_t kWB = SOLO ? 1u : (uint32_t)kWavesPerBlock;  // waves (LDS slots) per workgroup
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, LP = Shape<P>::LP, Q = Shape<P>::Q;
     constexpr uint32_t NPIX = 64u / LP;  // pixels traced at a time
+    constexpr bool kMergeable = Walk<WALK>::MERGEABLE;
     constexpr uint32_t kRing = Ring<LP>::N;
     extern __shared__ float4 smem[];
     // first launch of a key: the host has not read the live-tile count back, so
@@ -1327,8 +1330,11 @@ void trace_kernel(TraceArgs a) {
         if (alive == 0) break;
         const uint64_t st_t0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
         // Secondary segments run the full sphere loop; let them gather until
-        // enough lanes share one (or no primary work is ready).
-        const bool do_sec = sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
+        // enough lanes share one (or no primary work is ready).  Merged rounds
+        // (scenes of one or two groups, TraceArgs.merge_rounds): every round
+        // starts new samples AND continues paths, all through the exact loop.
+        const bool merged = kMergeable && a.merge_rounds != 0u;
+        const bool do_sec = !merged && sec != 0 && (pri == 0 || __builtin_popcountll(sec) >= a.sec_threshold);
         // (lazy: only when some lane waits for ring space, or nothing else is left)
         const bool fold_now = !do_sec && ((pri | sec) == 0 || (__builtin_amdgcn_ballot_w64(mode == 0u) & ~pri) != 0);
         if (fold_now) {
@@ -1342,6 +1348,7 @@ void trace_kernel(TraceArgs a) {
             can_start = mode == 0u && ring_ok;
             pri = LP == 1 ? __builtin_amdgcn_ballot_w64(mode == 0u) : ballot_and(mode == 0u, ring_ok);
         }
+        if (merged) pri |= sec;  // (the lanes a merged round traces)
         if ((pri | sec) != 0) {
             if (kStats && a.stats) {
                 if (do_sec) { st_sec_it += 1; st_sec_lanes += __builtin_popcountll(sec); }
@@ -1364,11 +1371,12 @@ void trace_kernel(TraceArgs a) {
             }
             // do_sec ? mode == 1 : can_start, as one compare against a uniform mode
             // and a uniform override of the ring test (no lane-mask select)
-            const bool traces = mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
+            const bool traces = merged ? (mode == 0u && ring_ok) || mode == 1u
+                                       : mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
             if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
             if (traces) {
                 pseg += 1u;
-                if (!do_sec) start_sample(kernel_args(), x, y, a.prev_count + k, p);
+                if (!do_sec && mode == 0u) start_sample(kernel_args(), x, y, a.prev_count + k, p);
                 bool done;
                 if (a.max_bounce == 0) {
                     done = true;  // no segment is traced; the frame folds black
@@ -1376,7 +1384,7 @@ void trace_kernel(TraceArgs a) {
                     Hit h;
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
-                    if (CULL && !do_sec) {
+                    if (CULL && !do_sec && !merged) {
                         for (uint32_t w = 0; w < n_words; ++w) {
                             // (readfirstlane returns int: widen each half as u32, or
                             // bit 31 would sign-extend into groups 32..63)

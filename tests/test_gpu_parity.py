@@ -382,7 +382,9 @@ VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0
                 {"RT_SOLO": "0"}, {"RT_SOLO": "0", "RT_CLUSTERS": "2"}, {"RT_WALK_ANY": "1"},
                 {"RT_WALK_ANY": "1", "RT_CLUSTERS": "2"}, {"RT_LANES_PER_PIXEL": "16", "RT_CLUSTERS": "2"},
                 # 4 pixels per lane at every frame count (the one-frame launch shape), and never
-                {"RT_LANES_PER_PIXEL": "1", "RT_PIXELS_PER_LANE": "4"}, {"RT_PIXELS_PER_LANE": "1"}]
+                {"RT_LANES_PER_PIXEL": "1", "RT_PIXELS_PER_LANE": "4"}, {"RT_PIXELS_PER_LANE": "1"},
+                # merged primary/secondary rounds forced on (every per-group-walk kernel) and off
+                {"RT_MERGE_ROUNDS": "1", "RT_CLUSTERS": "0"}, {"RT_MERGE_ROUNDS": "0"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
