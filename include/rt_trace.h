@@ -246,8 +246,8 @@ typedef struct rt_trace_info {
     uint32_t PixelsPerLane;   /* 4: each lane traced 4 pixels in turn (one-lane-
                                  per-pixel launches of one frame), else 1     */
     uint32_t PixelsSorted;    /* 1: the block tiles' pixels were dealt to their
-                                 waves by the previous launch's costs
-                                 (RT_PIXEL_SORT=1)                           */
+                                 waves by the previous launch's costs (P >= 4;
+                                 RT_PIXEL_SORT=0 disables)                   */
     uint32_t BufferGrowths;   /* launch-buffer (re)allocations on this device
                                  so far (tile lists, cull masks): constant
                                  across launches that rt_device_reserve covers */

@@ -1,6 +1,24 @@
+# Scheduling counters of the -DRTK_STATS build (make -C simd-ray-tracer_amd variant NAME=stats KFLAGS=-DRTK_STATS)
+# for each ';'-separated env variant in $VARIANTS and each bench config in $CONFIGS (';'-separated, "c2" = defaults).
+# Prints the lane-trip shares: done (finished lanes), primary/secondary lanes per round.
 set -o pipefail
 mkdir -p gpurun_out
-for cfg in "RT_STATS=1 RT_CULL=1 RT_SEC_THRESHOLD=16" "RT_STATS=1 RT_CULL=1 RT_SEC_THRESHOLD=1" "RT_STATS=1 RT_CULL=0 RT_SEC_THRESHOLD=1"; do
-  env $cfg timeout -k 10 120 python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/b.json 2> gpurun_out/b.err || exit $?
-  python -c "import json,sys; d=json.load(open('gpurun_out/b.json')); print('$cfg', d['value'], d['roofline']['kernel_ms'], d.get('sched_stats'))"
+IFS=';' read -ra VAR <<< "${VARIANTS:-RT_X=0}"
+IFS=';' read -ra CFG <<< "${CONFIGS:-c2}"
+for v in "${VAR[@]}"; do
+  for c in "${CFG[@]}"; do
+    args=$c; [ "$c" = "c2" ] && args=""
+    env RT_STATS=1 RT_TRACE_LIB=librt_trace_stats.so $v timeout -k 10 180 python bench.py --steps 1 --warmup ${WARMUP:-6} \
+      --no-cpu-baseline $args > gpurun_out/st.json 2> gpurun_out/st.err || { tail -5 gpurun_out/st.err; exit 1; }
+    python - "$v" "$c" <<'PY'
+import json, sys
+d = json.loads([l for l in open("gpurun_out/st.json") if l.startswith("{")][-1])
+s = d.get("sched_stats") or {}
+trips = s.get("pri_iters", 0) + s.get("sec_iters", 0)
+print(f"[{sys.argv[1]}] [{sys.argv[2]}] {d.get('value')} Mrays/s; trips {trips}; done lane-trips share "
+      f"{s.get('done_lane_trips', 0) / max(64 * trips, 1):.3f}; primary lanes/round {s.get('pri_lanes', 0) / max(s.get('pri_iters', 1), 1):.1f}; "
+      f"secondary lanes/round {s.get('sec_lanes', 0) / max(s.get('sec_iters', 1), 1):.1f}", flush=True)
+print("  ", json.dumps(s), flush=True)
+PY
+  done
 done

@@ -384,7 +384,7 @@ VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0
                 # 4 pixels per lane at every frame count (the one-frame launch shape), and never
                 {"RT_LANES_PER_PIXEL": "1", "RT_PIXELS_PER_LANE": "4"}, {"RT_PIXELS_PER_LANE": "1"},
                 # merged primary/secondary rounds forced on (every per-group-walk kernel) and off
-                {"RT_MERGE_ROUNDS": "1", "RT_CLUSTERS": "0"}, {"RT_MERGE_ROUNDS": "0"}]
+                {"RT_MERGE_ROUNDS": "1", "RT_CLUSTERS": "0"}, {"RT_MERGE_ROUNDS": "0"}, {"RT_PIXEL_SORT": "0"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
