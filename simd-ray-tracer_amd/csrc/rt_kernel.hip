@@ -1144,9 +1144,16 @@ void trace_kernel(TraceArgs a) {
     // owner lanes of in-image pixels (they fold until every frame is folded)
     const uint64_t folding = ballot_and(owner, valid);
     // lane mode: 0 = next sample pending, 1 = path continues (secondary), 2 = no samples left
+    // The P lanes of a pixel take its samples in order as they free up (kDynamic):
+    // each trip the lanes wanting a sample are ranked inside the slice and take
+    // next, next + 1, ...  A lane whose samples run short no longer idles while its
+    // neighbours trace theirs: only the pixel's last few samples leave lanes idle.
+    constexpr bool kDynamic = LP > 1;
     uint32_t k = j;            // this lane's next (or current) sample
+    uint32_t next = 0;         // kDynamic: the pixel's first unassigned sample (same on its lanes)
     uint32_t folded = 0;       // owner: samples folded so far
     uint32_t mode = (valid && k < a.frames) ? 0u : 2u;
+    const uint32_t slice_base = lane - j;
 
     uint64_t nrays = 0;  // wave total (uniform): segments traced by this wave
     uint32_t pseg = 0;   // segments this lane traced (pix_cost)
@@ -1248,7 +1255,8 @@ void trace_kernel(TraceArgs a) {
     // -- a DPP reduction inside the lane slice (quads, half rows, rows; a
     // cross-row shuffle only for P = 32), run with every lane active.
     auto parked_frontier = [&]() -> uint32_t {
-        uint32_t f = k;
+        // (kDynamic: samples below next are all assigned; those not in flight are parked)
+        uint32_t f = kDynamic && mode != 1u ? next : k;
 #define RTK_DMIN(CTRL) f = min(f, (uint32_t)__builtin_amdgcn_update_dpp((int)f, (int)f, CTRL, 0xf, 0xf, false))
         if (LP >= 2) RTK_DMIN(0xB1);   // quad_perm 1,0,3,2 (lane ^ 1)
         if (LP >= 4) RTK_DMIN(0x4E);   // quad_perm 2,3,0,1 (lane ^ 2)
@@ -1319,6 +1327,15 @@ void trace_kernel(TraceArgs a) {
         // unfolded sample's lane is never blocked, so this cannot deadlock)
         // the pixel's owner lane (first of its P-lane quad slice) via DPP
         uint32_t folded_g = fold_cursor();
+        uint32_t want_n = 0;  // kDynamic: the slice's lanes wanting a sample
+        if (kDynamic) {
+            const uint32_t sw_bits = (uint32_t)((__builtin_amdgcn_ballot_w64(mode == 0u) >> slice_base) & ((1ull << LP) - 1ull));
+            want_n = __builtin_popcount(sw_bits);
+            if (mode == 0u) {
+                k = next + __builtin_popcount(sw_bits & ((1u << j) - 1u));
+                if (k >= a.frames) mode = 2u;
+            }
+        }
         // (lane masks from single compares: see ballot_and)
         bool ring_ok = LP == 1 || k < folded_g + kRing;
         bool can_start = mode == 0u && ring_ok;
@@ -1374,6 +1391,8 @@ void trace_kernel(TraceArgs a) {
             const bool traces = merged ? (mode == 0u && ring_ok) || mode == 1u
                                        : mode == (do_sec ? 1u : 0u) && (do_sec || ring_ok);
             if (a.max_bounce != 0) nrays += __builtin_popcountll(do_sec ? sec : pri);
+            // the slice's lanes that start now are its lowest-ranked wanting ones
+            if (kDynamic && !do_sec) next = min(next + want_n, min(a.frames, folded_g + kRing));
             if (traces) {
                 pseg += 1u;
                 if (!do_sec && mode == 0u) start_sample(kernel_args(), x, y, a.prev_count + k, p);
@@ -1497,8 +1516,8 @@ void trace_kernel(TraceArgs a) {
                         if (__builtin_expect(k >= fold_n, 0)) w = fold_weights(a.prev_count + k);
                         ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
-                    k += LP;
-                    mode = k < a.frames ? 0u : 2u;
+                    k += kDynamic ? 0u : LP;
+                    mode = kDynamic || k < a.frames ? 0u : 2u;
                     if (Q > 1 && mode == 2u) {
                         // the pixel is complete: store it and move to the lane's next pixel
                         // slot inside the image (its samples start from k = 0)
