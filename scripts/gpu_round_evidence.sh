@@ -11,6 +11,8 @@ tail -c 400 gpurun_out/ev_${tag}_bench.json; echo
 TAG=ev_${tag}_trace bash scripts/gpu_trace_launches.sh > gpurun_out/ev_${tag}_launches.txt 2>&1 || { tail -5 gpurun_out/ev_${tag}_launches.txt; exit 1; }
 bash scripts/gpu_pmc.sh ev_${tag} > gpurun_out/ev_${tag}_pmc_stdout.txt 2>&1 || { tail -5 gpurun_out/ev_${tag}_pmc_stdout.txt; exit 1; }
 python scripts/pmc_to_json.py gpurun_out pmc_ev_${tag}_ gpurun_out/ev_${tag}_c2_pmc.json "C2: 1920x1080, 256 spp, 64 spheres, 8 bounces, SIMD rules" || exit 1
+bash scripts/gpu_pmc.sh ev_${tag}rtw --config rtw > gpurun_out/ev_${tag}_rtw_pmc_stdout.txt 2>&1 || { tail -5 gpurun_out/ev_${tag}_rtw_pmc_stdout.txt; exit 1; }
+python scripts/pmc_to_json.py gpurun_out pmc_ev_${tag}rtw_ gpurun_out/ev_${tag}_rtw_pmc.json "RTW: 1920x1080, 64 spp, 482 spheres, 8 bounces, SIMD rules, RTWeekend" || exit 1
 bash scripts/gpu_simranks_all.sh 8 > gpurun_out/ev_${tag}_simranks8.txt 2>&1 || exit 1
 for cfg in c3 rtw c2in; do
   timeout -k 10 300 python bench.py --config $cfg --steps 3 --warmup 3 --no-cpu-baseline >> gpurun_out/ev_${tag}_configs.jsonl 2>> gpurun_out/ev_${tag}_configs.err || exit 1
