@@ -1102,7 +1102,9 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     // Lanes per pixel (measured on MI355X at 1/2/4/8-way band splits of C2,
     // bench.py --sim-ranks, heaviest-first order at every P): 4 while the band
-    // has >= 6k pixels per CU, 8 down to 1.5k, else 16 (more lanes per pixel
+    // has >= 6k pixels per CU, 8 down to 3k, else 16 (round 4, with the in-pixel
+    // sample hand-out: the 4-rank share 1.19-1.23 ms at P = 16 against 1.25-1.28
+    // at P = 8; the 2-rank share 2.26-2.27 at P = 8, 2.29 at P = 16; more lanes per pixel
     // shorten the per-lane sample chains that form the launch tail; C2 rank
     // shares: 1 GPU P=4 6.21 ms (P=8 6.29, P=16 6.62); 2 ranks P=8 3.26 ms
     // (P=4 3.35); 4 ranks P=8 = P=16 1.81 ms; 8 ranks P=16 1.02 ms (P=8
@@ -1111,7 +1113,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     const bool auto_lpp = lpp == 0;
     if (lpp == 0) {
         const uint64_t pixels = (uint64_t)desc->Width * local_rows;
-        lpp = pixels >= (uint64_t)d->cu_count * 6144u ? 4 : pixels >= (uint64_t)d->cu_count * 1536u ? 8 : 16;
+        lpp = pixels >= (uint64_t)d->cu_count * 6144u ? 4 : pixels >= (uint64_t)d->cu_count * 3072u ? 8 : 16;
         while (lpp > 1 && (uint32_t)lpp / 2u >= desc->Frames) lpp /= 2;
     }
     // One lane per pixel, and one frame (the reference's OnRender unit): each lane
