@@ -391,6 +391,7 @@ def main_multi_device(args):
     c_last = max(args.warmup - 1, 0)
     rays_per_step = int(ctr[c_last].item())
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    growths0 = [multi.shard_info(i)["BufferGrowths"] for i in range(len(devices))]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -405,6 +406,7 @@ def main_multi_device(args):
         raise SystemExit(f"bench.py: timed steps counted {timed} segments, expected {rays_per_step} each")
     per_dev_ms = multi.last_trace_ms(len(devices))
     gather_ms = multi.last_gather_ms()
+    growths = sum(multi.shard_info(i)["BufferGrowths"] - g for i, g in enumerate(growths0))
     minfo = multi.info()
     call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     frame = full.clone()
@@ -433,6 +435,8 @@ def main_multi_device(args):
                       "note": "last timed call: from every device's trace done to the frame assembled on devices[0] "
                               "(HIP events on its gather stream: band transfer + scatter, rt_multi_last_gather_ms)"}
     line["call_ms_events"] = round(call_ms, 3)
+    # launch-buffer (re)allocations during the timed calls, over every device (rt_multi_reserve sized them: 0)
+    line["buffer_growths_timed"] = growths
     line["one_gpu"] = {"ms_per_frame": round(one_ms, 3), "device": d0,
                        "speedup_vs_one_gpu": round(one_ms / (elapsed / args.steps * 1e3), 3),
                        "note": "the same frame traced whole on devices[0] alone, in this run"}
