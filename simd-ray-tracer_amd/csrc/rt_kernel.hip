@@ -924,9 +924,9 @@ struct Ring {
 #define RTK_MIN_WAVES_PER_SIMD 7   // 7 waves = 72 VGPRs, no VGPR spills: measured best on C2 with the
 #endif                             // cluster walk (w6 116.5k, w7 120.0-121.1k, w8 118.2k Mrays/s, w8 spills)
 
-// Work shape.  A wave owns a small pixel tile and P lanes per pixel: lane
-// j of a pixel traces that pixel's samples k = j, j+P, j+2P, ... (any order
-// across lanes), parks each finished sample's radiance in a per-pixel LDS
+// Work shape.  A wave owns a small pixel tile and P lanes per pixel: the
+// lanes of a pixel take its samples in order as they free up (kDynamic in
+// trace_kernel), park each finished sample's radiance in a per-pixel LDS
 // ring, and the pixel's owner lane (j == 0) folds the ring into the running
 // mean strictly in sample order (main.cpp:484-487), so results are
 // bit-identical to one lane tracing the samples one after another.  P > 1
