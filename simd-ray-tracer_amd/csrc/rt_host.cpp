@@ -1093,10 +1093,13 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // secondary round (cluster pairs, or groups without clusters), the more it
     // pays to fill it first.  Measured (same box, Mrays/s, threshold 16/32/40/48):
     // RTWeekend (20 cluster pairs) 18.6k/19.4k/19.5k/19.5k, C5 at 512 spp (16)
-    // 44.7k/46.3k/46.4k/46.4k, C2 (5) 153.8k/151.2k/150.4k/149.9k.
+    // 44.7k/46.3k/46.4k/46.4k, C2 (5) 153.8k/151.2k/150.4k/149.9k.  Round 4 (in-pixel
+    // sample hand-out, 40/44/48/52): RTWeekend (per-lane thresholds) 25.61k/25.73k/25.74k/
+    // 25.71k, C5 (scene-wide) 52.74k/52.44k/52.58k/52.38k: 48 for per-lane walks.
     a.merge_rounds = d->merge_env == 1 || (d->merge_env == -1 && d->n_groups[rs] <= kMergeGroups) ? 1u : 0u;
     a.sec_threshold = d->sec_threshold;
-    if (a.sec_threshold == 0) a.sec_threshold = (a.clusters ? a.n_cpairs : a.n_groups) >= 12u ? 40u : 16u;
+    if (a.sec_threshold == 0)
+        a.sec_threshold = (a.clusters ? a.n_cpairs : a.n_groups) >= 12u ? (a.pf_relative ? 48u : 40u) : 16u;
     a.stats = d->d_stats;
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
