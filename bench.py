@@ -112,6 +112,49 @@ def make_scene(rt, args):
     return scene
 
 
+GOLDEN = ROOT / "tests" / "golden" / "oracle_regression.json"
+
+
+def golden_for(args, W, H, S, N, B):
+    """The committed fixture of this exact workload (tests/golden/oracle_regression.json;
+    every pixel-mode entry there was also rendered by the reference itself,
+    tests/golden/reference_frames.json "pixel_cases"), or None."""
+    try:
+        gold = json.loads(GOLDEN.read_text())
+    except (OSError, ValueError):
+        return None, None
+    for name, g in gold.items():
+        if (g.get("seed_mode") == "pixel" and g["scene"] == args.scene and g["width"] == W and g["height"] == H
+                and g["frames"] == S and g["bounces"] == B and g["simd"] == (not args.scalar)
+                and (g["spheres"] is None or g["spheres"] == N) and g.get("distance") == args.distance):
+            return name, g
+    return None, None
+
+
+def check_frame(rt, args, W, H, S, N, B, cur_host, prev_host, rays):
+    """Hashes the last timed frame (RGBA8 and, when given, the v4 running mean)
+    with the library's rt_frame_hash and compares it with the committed
+    fixture: {"verified": bool or None, "golden": name, ...}."""
+    name, g = golden_for(args, W, H, S, N, B)
+    if g is None:
+        return {"verified": None, "golden": None, "note": "no committed fixture for this workload"}
+    got = {"rgba8": f"{rt.frame_hash(cur_host):016x}", "rays": rays}
+    ok = got["rgba8"] == g["fnv1a64_rgba8"] and rays == g["rays"]
+    if prev_host is not None:
+        got["v4"] = f"{rt.frame_hash(prev_host):016x}"
+        ok = ok and got["v4"] == g["fnv1a64_v4"]
+    return {"verified": bool(ok), "golden": f"tests/golden/oracle_regression.json:{name}",
+            "hashes": got, "expected": {"rgba8": g["fnv1a64_rgba8"], "v4": g["fnv1a64_v4"], "rays": g["rays"]},
+            "note": "FNV-1a 64 (rt_frame_hash) of the last timed frame copied to the host after timing; the fixture "
+                    "was rendered by the oracle and by the reference's own RenderTile (SURVEY 8c pixel mode)"}
+
+
+def combine_verified(vs_one_gpu, vs_golden):
+    """False if either check failed, True if one passed and none failed, None if neither ran."""
+    checks = [v for v in (vs_one_gpu, vs_golden) if v is not None]
+    return None if not checks else all(checks)
+
+
 def cpu_baseline(args, n_rays_gpu_step: int):
     """The oracle (C restatement of RenderTile, lane-4 SSE, pthread 32x32 tile
     queue) on this host's cores, on a bounded sample of the same workload:
@@ -415,6 +458,7 @@ def main_multi_device(args):
     dev.upload_scene(scene)
     ref, one_ms, one_rays = one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, min(args.steps, 5))
     verified = bool(torch.equal(frame, ref)) and one_rays == rays_per_step
+    frame_check = check_frame(rt, args, W, H, S, N, B, frame.cpu().numpy().view("uint32"), None, rays_per_step)
     workload = workload_name(args, W, H, S, N, B)
     gather = ("RCCL grouped send/recv to devices[0] (ncclCommInitAll) + rt_assemble scatter, overlapping the next "
               "call's traces" if minfo["Transport"] == rt.RT_MULTI_RCCL else
@@ -440,7 +484,9 @@ def main_multi_device(args):
     line["one_gpu"] = {"ms_per_frame": round(one_ms, 3), "device": d0,
                        "speedup_vs_one_gpu": round(one_ms / (elapsed / args.steps * 1e3), 3),
                        "note": "the same frame traced whole on devices[0] alone, in this run"}
-    line["verified"] = verified
+    line["verified_vs_one_gpu"] = verified
+    line["frame_check"] = frame_check
+    line["verified"] = combine_verified(verified, frame_check["verified"])
     # the roofline of the slowest device's share (its trace kernel; counters: the committed share record)
     slowest = max(range(len(devices)), key=lambda i: per_dev_ms[i])
     rows0 = rt.band_local_rows(H, band_rows, args.gpus, slowest)
@@ -451,6 +497,9 @@ def main_multi_device(args):
     print(json.dumps(line), flush=True)
     dev.close()
     multi.close()
+    if line["verified"] is False:
+        print(f"bench.py: the gathered frame does NOT match: {frame_check}", file=sys.stderr)
+        raise SystemExit(3)
 
 
 def main_onrender(args):
@@ -724,6 +773,13 @@ def main():
             verified = bool(torch.equal(got, ref_cur))
         if world > 1:
             dist.barrier()
+    frame_check = None
+    if rank == 0 and bands == world:
+        # the last timed frame against the committed fixture of this workload
+        last = full if world > 1 else cur[(state["n"] - 1) % 2]
+        torch.cuda.synchronize()
+        frame_check = check_frame(rt, args, W, H, S, args.spheres, B, last.cpu().numpy().view("uint32"),
+                                  prev.cpu().numpy() if world == 1 else None, int(rays_per_step[0].item()))
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     t = torch.tensor([elapsed, kern_ms, cold_ms], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -769,10 +825,17 @@ def main():
         if stats:
             line["sched_stats"] = stats
         if verified is not None:
-            line["verified"] = verified
+            line["verified_vs_one_gpu"] = verified
+        if frame_check is not None:
+            line["frame_check"] = frame_check
+            line["verified"] = combine_verified(verified, frame_check["verified"])
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, total_rays)
         print(json.dumps(line), flush=True)
+        if line.get("verified") is False:
+            print(f"bench.py: the timed frame does NOT match {frame_check.get('golden')}: {frame_check}",
+                  file=sys.stderr)
+            raise SystemExit(3)
     if comm:
         comm.close()
     dev.close()

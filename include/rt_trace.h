@@ -519,6 +519,13 @@ int rt_on_render_get_profile(rt_on_render_profile *out, int reset);
 int rt_image_write_ppm(const rt_image *image, const char *path, uint32_t flags);
 int rt_image_write_png(const rt_image *image, const char *path, uint32_t flags);
 
+/* FNV-1a 64 of `nbytes` host bytes (offset basis 0xcbf29ce484222325, prime
+ * 0x100000001b3): the frame checksum the committed fixtures hold
+ * (tests/golden, *.json), so a caller can check a rendered frame -- RGBA8 or
+ * the v4 running mean copied to the host -- against a golden without the
+ * checker.  New; the reference has no frame checksum. */
+uint64_t rt_frame_hash(const void *data, uint64_t nbytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,7 +29,28 @@ inline u32 f32x4::FindFirstIndex(const f32x4 &A, f32 Value) {
 inline f32 f32x4::Extract(u32 Index) { return (*this)[Index]; }
 inline u32 u32x4::Extract(u32 Index) { return (*this)[Index]; }
 
+#ifndef RT_REF_PATCHED
 #include "_ref/main_7_640.inc"   // main.cpp:7-640, verbatim
+#else
+// librefpix.so: the same lines with SURVEY §8c's two textual patches
+// (oracle/Makefile, _ref/main_7_640_px.inc): MaxRayBounce = RtMaxRayBounce at
+// main.cpp:387,536, and RT_PIXEL_SEED_HOOK(x, y) at the top of the pixel loops
+// (main.cpp:373,522).  With RtMaxRayBounce 5 and RtPixelSeeds 0 this build is
+// the verbatim one.  The pixel seed is OnInit's own mixer (main.cpp:668-675,
+// extracted verbatim) applied to i = (PreviousRayCount*H + y)*W + x, i.e.
+// SURVEY §8c's `pixel` seed mode; i is 64-bit (C3's index passes 2^32).
+static u32 RtMaxRayBounce = 5;
+static int RtPixelSeeds = 0;
+static u64 RtSeedMix(u64 i) {
+#include "_ref/main_668_675.inc"
+    return InitialSeed;
+}
+#define RT_PIXEL_SEED_HOOK(x, y)                                                                              \
+    if (RtPixelSeeds)                                                                                          \
+        RandomState.Seed = RtSeedMix(((u64)PreviousRayCount * CurrentImage.Height + (y)) * CurrentImage.Width + (x))
+#include "_ref/main_7_640_px.inc"  // main.cpp:7-640 with the two patches
+#include <pthread.h>
+#endif
 
 extern "C" {
 // ------------------------------------------------------- the math layer
@@ -142,7 +163,8 @@ int ref_scene_builtin(int index, void *spheres, u32 cap_spheres, void *groups, u
 // for frame k (OnRender, main.cpp:797-806).  The scene is the caller's arrays
 // (layouts identical to main.cpp:11-26); the camera is camera_info's first 92
 // bytes (main.cpp:270-278).  MaxRayBounce is the reference's literal 5
-// (main.cpp:387,536).  *state and *rays are updated.
+// (main.cpp:387,536) in librefmath.so, ref_set_patch's value in librefpix.so
+// (which also re-seeds per pixel when asked).  *state and *rays are updated.
 void ref_render(const void *spheres, u32 n_spheres, const void *groups, u32 n_groups, const void *materials,
                 u32 n_materials, u32 use_sky, const f32 *cam, u32 width, u32 height, u32 prev_count, u32 frames,
                 int simd, u64 *state, f32 *prev_v4, u32 *cur, u64 *rays) {
@@ -181,4 +203,73 @@ void ref_render(const void *spheres, u32 n_spheres, const void *groups, u32 n_gr
     Scenes[1] = Saved;
     SceneIndex = SavedIndex;
 }
+
+#ifdef RT_REF_PATCHED
+// The patched build's knobs: MaxRayBounce (patch i) and per-(pixel, frame)
+// seeds (patch ii).
+void ref_set_patch(u32 max_bounce, int pixel_seeds) { RtMaxRayBounce = max_bounce; RtPixelSeeds = pixel_seeds; }
+
+struct RtPool { u32 tiles; u32 simd; volatile u32 next; };
+static void *rt_worker(void *arg) {
+    void **a = (void **)arg;
+    RtPool *p = (RtPool *)a[0];
+    u32 index = (u32)(uintptr_t)a[1];
+    for (;;) {
+        u32 t = __atomic_fetch_add(&p->next, 1u, __ATOMIC_RELAXED);
+        if (t >= p->tiles) break;
+        work_queue_context Work = {};
+        Work.WorkEntry = t;
+        Work.ThreadIndex = index;
+        if (p->simd) RenderTile(&Work);
+        else RenderTileScalar(&Work);
+    }
+    return 0;
+}
+
+// ref_render with the tiles of each frame pulled by `threads` workers from
+// one counter, as the reference's work queue deals them (wasm/wasm.cpp:624-694,
+// main.cpp:851-856).  Only meaningful with pixel seeds on (the output is then
+// independent of the schedule); *rays is the sum over the workers.
+void ref_render_threads(const void *spheres, u32 n_spheres, const void *groups, u32 n_groups, const void *materials,
+                        u32 n_materials, u32 use_sky, const f32 *cam, u32 width, u32 height, u32 prev_count,
+                        u32 frames, int simd, u32 threads, f32 *prev_v4, u32 *cur, u64 *rays) {
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    static thread_context Context[64];
+    scene Saved = Scenes[1];
+    u32 SavedIndex = SceneIndex;
+    scene &S = Scenes[1];
+    S.UseSkyColor = use_sky != 0;
+    S.ScalarSpheres.Data = (scalar_sphere *)spheres; S.ScalarSpheres.Count = n_spheres;
+    S.SIMDSpheres.Data = (sphere_group *)groups;     S.SIMDSpheres.Count = n_groups;
+    S.Materials.Data = (material *)materials;        S.Materials.Count = n_materials;
+    SceneIndex = 1;
+    __builtin_memcpy(&CameraInfo, cam, 92);
+    CameraInfo.TilesX = (width + TileSize - 1) / TileSize;
+    CameraInfo.CurrentImage.Data = cur;      CameraInfo.CurrentImage.Width = width;  CameraInfo.CurrentImage.Height = height;
+    CameraInfo.PreviousImage.Data = prev_v4; CameraInfo.PreviousImage.Width = width; CameraInfo.PreviousImage.Height = height;
+    for (u32 i = 0; i < threads; ++i) { Context[i].RandomState.Seed = 0; Context[i].RaysCastInThread = 0; }
+    ThreadContexts = Context;
+    RtPool pool;
+    pool.tiles = CameraInfo.TilesX * ((height + TileSize - 1) / TileSize);
+    pool.simd = simd ? 1u : 0u;
+    pthread_t th[64];
+    void *args[64][2];
+    for (u32 k = 0; k < frames; ++k) {
+        PreviousRayCount = prev_count + k;
+        pool.next = 0;
+        for (u32 i = 0; i < threads; ++i) {
+            args[i][0] = &pool; args[i][1] = (void *)(uintptr_t)i;
+            pthread_create(&th[i], 0, rt_worker, args[i]);
+        }
+        for (u32 i = 0; i < threads; ++i) pthread_join(th[i], 0);
+    }
+    u64 total = 0;
+    for (u32 i = 0; i < threads; ++i) total += Context[i].RaysCastInThread;
+    *rays = total;
+    ThreadContexts = 0;
+    Scenes[1] = Saved;
+    SceneIndex = SavedIndex;
+}
+#endif
 }

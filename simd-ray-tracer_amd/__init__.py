@@ -168,6 +168,7 @@ SIGNATURES = {
     "rt_on_render_get_profile": (c_int, [POINTER(RtOnRenderProfile), c_int]),
     "rt_image_write_ppm": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
     "rt_image_write_png": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
+    "rt_frame_hash": (c_uint64, [c_void_p, c_uint64]),
 }
 
 _LIB: Optional[ctypes.CDLL] = None
@@ -604,3 +605,9 @@ def write_image(image: np.ndarray, path, flip_y: bool = True) -> None:
     fn = lib().rt_image_write_png if path.lower().endswith(".png") else lib().rt_image_write_ppm
     name = "rt_image_write_png" if path.lower().endswith(".png") else "rt_image_write_ppm"
     _check(fn(ctypes.byref(img), path.encode(), RT_IMAGE_FLIP_Y if flip_y else 0), name)
+
+
+def frame_hash(a) -> int:
+    """FNV-1a 64 of a host array's bytes (rt_frame_hash): the golden fixtures' frame checksum."""
+    a = np.ascontiguousarray(a)
+    return int(lib().rt_frame_hash(c_void_p(a.ctypes.data), a.nbytes))

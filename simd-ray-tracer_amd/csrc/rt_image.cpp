@@ -116,3 +116,14 @@ extern "C" int rt_image_write_png(const rt_image *image, const char *path, uint3
     ok = (fclose(f) == 0) && ok;
     return ok ? RT_OK : RT_EIO;
 }
+
+extern "C" uint64_t rt_frame_hash(const void *data, uint64_t nbytes) {
+    const unsigned char *p = static_cast<const unsigned char *>(data);
+    uint64_t h = 0xcbf29ce484222325ull;
+    if (!p) return h;
+    for (uint64_t i = 0; i < nbytes; ++i) {
+        h ^= p[i];
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}

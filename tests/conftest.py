@@ -142,6 +142,27 @@ def refmath():
 
 
 @pytest.fixture(scope="session")
+def refpix():
+    """The reference's main.cpp:7-640 with SURVEY §8c's two textual patches
+    (bounce count, per-pixel seeds) on a temporary copy (`make -C oracle ref`,
+    oracle/_ref/librefpix.so); only present in the build container."""
+    import ctypes
+    path = ROOT / "oracle" / "_ref" / "librefpix.so"
+    if not path.exists():
+        pytest.skip("oracle/_ref/librefpix.so not built (needs /root/reference)")
+    L = ctypes.CDLL(str(path))
+    v, u32 = ctypes.c_void_p, ctypes.c_uint32
+    L.ref_set_patch.restype = None
+    L.ref_set_patch.argtypes = [u32, ctypes.c_int]
+    L.ref_render.restype = None
+    L.ref_render.argtypes = [v, u32, v, u32, v, u32, u32, v, u32, u32, u32, u32, ctypes.c_int, v, v, v, v]
+    L.ref_render_threads.restype = None
+    L.ref_render_threads.argtypes = [v, u32, v, u32, v, u32, u32, v, u32, u32, u32, u32, ctypes.c_int, u32, v, v, v]
+    yield L
+    L.ref_set_patch(5, 0)
+
+
+@pytest.fixture(scope="session")
 def torch_cuda():
     import torch
     if not torch.cuda.is_available():

@@ -29,6 +29,15 @@ CASES = [
     ("rtweekend_80x48x2_scalar", 2, None, 80, 48, 2, 5, False, "pixel"),
     ("ragged_n13_37x23x3", 1, 13, 37, 23, 3, 6, True, "pixel"),
     ("survey_scene1_stream_256x4", 1, None, 256, 256, 4, 5, True, "stream"),
+    # round 5: the parity mode at B = 8 on the colour scenes and the scalar rules at
+    # B = 8 / 16 -- these, like every pixel case, are also rendered by the reference
+    # itself (tests/golden/make_reference_golden.py, SURVEY 8c patches)
+    ("rgb_glass_b8_96x64x4", 0, None, 96, 64, 4, 8, True, "pixel"),
+    ("rgb_glass_b8_96x64x4_scalar", 0, None, 96, 64, 4, 8, False, "pixel"),
+    ("rtweekend_b8_80x48x2", 2, None, 80, 48, 2, 8, True, "pixel"),
+    ("rtweekend_b8_80x48x2_scalar", 2, None, 80, 48, 2, 8, False, "pixel"),
+    ("n64_b8_128x96x8_scalar", 1, 64, 128, 96, 8, 8, False, "pixel"),
+    ("n256_b16_64x64x2_scalar", 1, 256, 64, 64, 2, 16, False, "pixel"),
     ("survey_n64_pixel_256x4", 1, 64, 256, 256, 4, 8, True, "pixel"),
     # BASELINE.json configs[1] (C2) at full size: the whole 1920x1080 frame, 256 spp
     ("c2_full_1920x1080x256", 1, 64, 1920, 1080, 256, 8, True, "pixel"),

@@ -10,12 +10,23 @@ tests/test_oracle_vs_reference_render.py check the oracle against the
 reference where /root/reference is absent.  Needs an Intel host (the
 reference's NormalizeFast is the host's rsqrtss).
 
-    python tests/golden/make_reference_golden.py
+Round 5 adds "pixel_cases": every pixel-seed case of
+tests/golden/oracle_regression.json (the fixtures the GPU path is checked
+against, tests/test_golden_regression.py), rendered by the reference itself in
+SURVEY §8c's `pixel` mode at the case's bounce count -- main.cpp:7-640 with the
+two textual patches on a temporary copy (oracle/Makefile, librefpix.so) --
+including the full BASELINE frames (C2, C3, RTWeekend, C2 from inside).  The
+patched build runs the reference's tiles on a pthread pool (the output is
+schedule-independent in pixel mode).
+
+    python tests/golden/make_reference_golden.py [--pixel-only] [--skip-c3]
 """
 import ctypes
 import json
+import os
 import pathlib
 import sys
+import time
 
 import numpy as np
 
@@ -24,6 +35,8 @@ sys.path.insert(0, str(ROOT))
 from oracle import oracle as orc  # noqa: E402  (scene/camera inputs and the FNV hash only)
 
 OUT = pathlib.Path(__file__).with_name("reference_frames.json")
+PIXEL_SOURCE = ("/root/reference/main.cpp:7-640 with SURVEY 8c's patches (MaxRayBounce :387,536; per-pixel seed "
+                "after :373,522 with the mixer of :668-675) via oracle/ref_harness.cpp -DRT_REF_PATCHED")
 
 # (name, builtin scene, sphere prefix or None, W, H, frames, simd, prev_count)
 CASES = [
@@ -45,7 +58,50 @@ def scene_of(index, prefix):
     return o.prefix(prefix) if prefix else o
 
 
+def pixel_cases(skip_c3: bool) -> dict:
+    """Every pixel-mode case of oracle_regression.json, rendered by librefpix.so."""
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_golden
+    P = ctypes.CDLL(str(ROOT / "oracle" / "_ref" / "librefpix.so"))
+    v, u32 = ctypes.c_void_p, ctypes.c_uint32
+    P.ref_set_patch.argtypes = [u32, ctypes.c_int]
+    P.ref_render_threads.argtypes = [v, u32, v, u32, v, u32, u32, v, u32, u32, u32, u32, ctypes.c_int, u32, v, v, v]
+    threads = min(8, os.cpu_count() or 1)
+    out = {}
+    for name, idx, n, w, h, frames, bounces, simd, seed in make_golden.CASES:
+        if seed != "pixel" or (skip_c3 and name in make_golden.SLOW):
+            continue
+        o = scene_of(idx, n)
+        cam = orc.camera(o, w, h, distance=make_golden.DISTANCE.get(name))
+        prev = np.zeros((w * h, 4), np.float32)
+        cur = np.zeros(w * h, np.uint32)
+        rays = np.zeros(1, np.uint64)
+        P.ref_set_patch(bounces, 1)
+        t = time.time()
+        P.ref_render_threads(o.spheres.ctypes.data, len(o.spheres), o.groups.ctypes.data, len(o.groups),
+                             o.materials.ctypes.data, len(o.materials), int(o.use_sky), cam.ctypes.data, w, h, 0,
+                             frames, int(simd), threads, prev.ctypes.data, cur.ctypes.data, rays.ctypes.data)
+        out[name] = {"scene": idx, "spheres": n, "width": w, "height": h, "frames": frames, "bounces": bounces,
+                     "simd": simd, **({"distance": make_golden.DISTANCE[name]} if name in make_golden.DISTANCE else {}),
+                     "rays": int(rays[0]), "fnv1a64_rgba8": f"{orc.fnv1a64(cur):016x}",
+                     "fnv1a64_v4": f"{orc.fnv1a64(prev):016x}", "ref_seconds": round(time.time() - t, 2),
+                     "ref_threads": threads}
+        print(name, out[name]["rays"], out[name]["fnv1a64_rgba8"], out[name]["ref_seconds"], "s", flush=True)
+    return out
+
+
 def main():
+    keep = json.loads(OUT.read_text()) if OUT.exists() else {}
+    pixel_only = "--pixel-only" in sys.argv
+    px = pixel_cases("--skip-c3" in sys.argv)
+    if "--skip-c3" in sys.argv:  # keep a previously rendered C3 entry
+        for k, e in keep.get("pixel_cases", {}).items():
+            px.setdefault(k, e)
+    if pixel_only:
+        keep["pixel_cases"] = px
+        keep["pixel_source"] = PIXEL_SOURCE
+        OUT.write_text(json.dumps(keep, indent=1) + "\n")
+        return
     L = ctypes.CDLL(str(ROOT / "oracle" / "_ref" / "librefmath.so"))
     v, u32 = ctypes.c_void_p, ctypes.c_uint32
     L.ref_render.argtypes = [v, u32, v, u32, v, u32, u32, v, u32, u32, u32, u32, ctypes.c_int, v, v, v, v]
@@ -68,7 +124,8 @@ def main():
         print(name, out[name]["rays"], out[name]["rgba8_fnv1a64"])
     OUT.write_text(json.dumps({"generator": "tests/golden/make_reference_golden.py",
                                "source": "/root/reference/main.cpp:7-640 via oracle/ref_harness.cpp",
-                               "max_bounce": 5, "cases": out}, indent=1) + "\n")
+                               "max_bounce": 5, "cases": out, "pixel_source": PIXEL_SOURCE, "pixel_cases": px},
+                              indent=1) + "\n")
 
 
 if __name__ == "__main__":

@@ -302,3 +302,130 @@ def test_oracle_matches_reference_golden_frames(orc, name, case):
     assert f"{int(st[0]):016x}" == case["final_state"]
     assert f"{orc.fnv1a64(cur):016x}" == case["rgba8_fnv1a64"]
     assert f"{orc.fnv1a64(prev):016x}" == case["v4_fnv1a64"]
+
+
+# -------------------- the parity mode itself: SURVEY 8c's patched reference
+# librefpix.so is main.cpp:7-640 with SURVEY 8c's two textual patches applied to
+# a temporary copy by oracle/Makefile: (i) MaxRayBounce reads a harness global
+# (main.cpp:387,536), (ii) the pixel loops re-seed the thread's PCG with
+# OnInit's mixer (main.cpp:668-675) at i = (PreviousRayCount*H + y)*W + x
+# (after main.cpp:373,522).  That is the `pixel` seed mode and the bounce
+# counts the GPU is held to.
+sys_path_golden = str(GOLDEN.parent)
+
+
+def _make_golden():
+    import sys
+    if sys_path_golden not in sys.path:
+        sys.path.insert(0, sys_path_golden)
+    import make_golden
+    return make_golden
+
+
+def _refpix_render(refpix, o, cam, w, h, frames, simd, bounces, threads=0, prev_count=0, prev=None, seed=None):
+    prev = np.zeros((w * h, 4), F) if prev is None else prev.copy()
+    cur = np.zeros(w * h, np.uint32)
+    rays = np.zeros(1, np.uint64)
+    args = (o.spheres.ctypes.data, len(o.spheres), o.groups.ctypes.data, len(o.groups), o.materials.ctypes.data,
+            len(o.materials), int(o.use_sky), cam.ctypes.data, w, h, prev_count, frames, int(simd))
+    st = np.array([seed if seed is not None else 0], np.uint64)
+    if threads:
+        refpix.ref_render_threads(*args, threads, prev.ctypes.data, cur.ctypes.data, rays.ctypes.data)
+    else:
+        refpix.ref_render(*args, st.ctypes.data, prev.ctypes.data, cur.ctypes.data, rays.ctypes.data)
+    return prev, cur, int(rays[0]), int(st[0])
+
+
+@pytest.mark.parametrize("simd", [True, False], ids=["RenderTile", "RenderTileScalar"])
+def test_patched_reference_is_neutral_at_five_bounces(orc, refmath, refpix, simd):
+    """With MaxRayBounce 5 and pixel seeds off, the patched build renders the
+    verbatim build's frames: same v4, RGBA8, ray count and final PCG state
+    (stream mode, so every draw of the thread's one PCG stream is compared)."""
+    refpix.ref_set_patch(5, 0)
+    for idx, n, (w, h), frames in ((1, None, (256, 256), 4), (0, None, (96, 64), 3), (2, None, (96, 64), 2),
+                                   (1, 13, (70, 33), 2)):
+        o = orc.scene_builtin(idx)
+        o = o.prefix(n) if n else o
+        cam = orc.camera(o, w, h)
+        seed = orc.seed_mix(idx)
+        a = _ref_render(refmath, o, cam, w, h, frames, simd, seed)
+        b = _refpix_render(refpix, o, cam, w, h, frames, simd, 5, seed=seed)
+        assert np.array_equal(_u(a[0]), _u(b[0])) and np.array_equal(a[1], b[1]), (idx, n)
+        assert (a[2], a[3]) == (b[2], b[3]), (idx, n, a[2:], b[2:])
+
+
+def _pixel_cases(max_rays=2_000_000):
+    mg = _make_golden()
+    gold = __import__("json").loads((GOLDEN.parent / "oracle_regression.json").read_text())
+    return [c for c in mg.CASES if c[8] == "pixel" and gold[c[0]]["rays"] <= max_rays]
+
+
+@intel_only
+@pytest.mark.parametrize("case", _pixel_cases(), ids=[c[0] for c in _pixel_cases()])
+def test_oracle_pixel_mode_vs_patched_reference(orc, refpix, case):
+    """The oracle's `pixel` seed mode -- the mode every GPU parity test and
+    BASELINE config runs -- against the reference's own RenderTile /
+    RenderTileScalar in that mode at the case's bounce count, bit for bit:
+    C1 (256^2, N=4, B=1), N=64 at B=8, N=256 at B=16, RGB Glass and RTWeekend
+    at B=5 and B=8, both rule sets, and SURVEY 8c's 341,802-segment probe."""
+    name, idx, n, w, h, frames, bounces, simd, _ = case
+    o = orc.scene_builtin(idx)
+    o = o.prefix(n) if n else o
+    cam = orc.camera(o, w, h, distance=_make_golden().DISTANCE.get(name))
+    refpix.ref_set_patch(bounces, 1)
+    rp, rc, rr, _ = _refpix_render(refpix, o, cam, w, h, frames, simd, bounces)
+    refpix.ref_set_patch(5, 0)
+    op, oc, orr = orc.render(o, cam, w, h, frames=frames, max_bounce=bounces, simd=simd, seed_mode=orc.SEED_PIXEL,
+                             threads=4)
+    assert rr == orr, (rr, orr)
+    bad = np.flatnonzero(np.any(_u(op) != _u(rp), axis=1))
+    assert bad.size == 0, ("v4", bad[:5], op[bad[:3]], rp[bad[:3]])
+    assert np.array_equal(oc, rc)
+    if name == "survey_n64_pixel_256x4":
+        assert rr == 341802  # SURVEY 8c's probe value, reproduced by the reference itself
+
+
+@intel_only
+def test_patched_reference_pixel_mode_continuation_and_threads(orc, refpix):
+    """A continued accumulation (PreviousRayCount 9, random non-zero mean) in
+    pixel mode, and the reference's tiles pulled by 1 or 5 worker threads (its
+    work queue, wasm/wasm.cpp:624-694): pixel seeds make the frame independent
+    of the schedule, and the oracle matches it."""
+    o = orc.scene_builtin(1).prefix(64)
+    w, h = 100, 70
+    cam = orc.camera(o, w, h)
+    prev = RNG.uniform(0, 1.5, (w * h, 4)).astype(F)
+    refpix.ref_set_patch(8, 1)
+    a = _refpix_render(refpix, o, cam, w, h, 3, True, 8, prev_count=9, prev=prev)
+    b = _refpix_render(refpix, o, cam, w, h, 3, True, 8, threads=5, prev_count=9, prev=prev)
+    c = _refpix_render(refpix, o, cam, w, h, 3, True, 8, threads=1, prev_count=9, prev=prev)
+    refpix.ref_set_patch(5, 0)
+    for x in (b, c):
+        assert np.array_equal(_u(a[0]), _u(x[0])) and np.array_equal(a[1], x[1]) and a[2] == x[2]
+    op, oc, orr = orc.render(o, cam, w, h, prev_count=9, frames=3, max_bounce=8, seed_mode=orc.SEED_PIXEL, threads=3,
+                             prev=prev.copy())
+    assert orr == a[2] and np.array_equal(_u(op), _u(a[0])) and np.array_equal(oc, a[1])
+
+
+def test_reference_pixel_frames_equal_the_gpu_fixtures():
+    """tests/golden/reference_frames.json "pixel_cases" were rendered by the
+    patched reference itself (make_reference_golden.py), including the full
+    BASELINE frames: C2 (1920x1080x256, N=64, B=8), C3 (3840x2160x1024), the
+    RTWeekend and inside-the-cloud frames.  Every one must equal the fixture of
+    the same name in oracle_regression.json, which the GPU path is checked
+    against (test_golden_regression.py::test_gpu_matches_golden) and bench.py
+    checks its timed frame against.  So reference == fixture == GPU, with no
+    live reference needed (this runs on any host)."""
+    import json
+    ref = json.loads(GOLDEN.read_text())["pixel_cases"]
+    gold = json.loads((GOLDEN.parent / "oracle_regression.json").read_text())
+    pixel = {k for k, g in gold.items() if g["seed_mode"] == "pixel"}
+    assert set(ref) == pixel, sorted(set(ref) ^ pixel)
+    for k in sorted(pixel):
+        r, g = ref[k], gold[k]
+        for f in ("scene", "spheres", "width", "height", "frames", "bounces", "simd", "rays", "fnv1a64_rgba8",
+                  "fnv1a64_v4"):
+            assert r[f] == g[f], (k, f, r[f], g[f])
+        assert r.get("distance") == g.get("distance"), k
+    for k in ("c2_full_1920x1080x256", "c3_full_3840x2160x1024", "rtw_full_1920x1080x64"):
+        assert k in ref
