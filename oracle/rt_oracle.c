@@ -531,6 +531,7 @@ static void trace_simd(const trace_ctx *c, uint32_t x, uint32_t y, uint64_t *rng
         __m128 min_t = _mm_set1_ps(OR_FMAX);
         __m128i grp = _mm_setzero_si128();
         __m128 inside = _mm_setzero_ps();
+#pragma clang loop unroll_count(2)  /* as main.cpp:398 */
         for (uint32_t g = 0; g < c->n_groups; ++g) {
             __m128 cx, cy, cz, t, dist, r2;
             group_core(&c->groups[g], ox, oy, oz, dx, dy, dz, &cx, &cy, &cz, &t, &dist, &r2);
