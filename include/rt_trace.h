@@ -258,9 +258,12 @@ int rt_trace_last_info(rt_device *dev, rt_trace_info *out);
  * cull pass's masks and counters) for bands of up to `width` x `local_rows`
  * pixels under every lanes-per-pixel shape rt_trace may pick, so that no later
  * rt_trace of such a band allocates or waits for the device (growing a buffer
- * otherwise synchronises the launch's stream).  Masks are sized for the
- * current scene; rt_scene_upload re-applies the reservation for a larger one.
- * Waits for the device.  (New; the reference's arena is sized once in OnInit,
+ * otherwise synchronises the launch's stream).  Successive calls keep the
+ * largest tile and pixel counts over the geometries asked for (not the largest
+ * width times the largest height).  Masks are sized for the current scene;
+ * rt_scene_upload re-applies the reservation for a larger one (if that fails,
+ * the upload still succeeds and the reservation is dropped: later launches
+ * grow their buffers as they need).  Waits for the device.  (New; the reference's arena is sized once in OnInit,
  * main.cpp:658.) */
 int rt_device_reserve(rt_device *dev, uint32_t width, uint32_t local_rows);
 
@@ -362,7 +365,10 @@ int rt_multi_shard_info(rt_multi *m, uint32_t index, rt_trace_info *out);
  * and devices[0]'s gather staging for frames up to width x height in
  * band_rows-row bands (0 = 8), so no rt_multi_trace of that geometry
  * allocates; RT_MULTI_RESERVE_MEAN also sizes the staging of the gathered
- * running mean (cam->PreviousImage).  Waits for the devices. */
+ * running mean (cam->PreviousImage).  Waits for the devices.  A reservation
+ * that grows the devices' resident running means discards them: the next
+ * call must restart the mean (PreviousRayCount 0 or RT_FLAG_ACCUM_ZERO), a
+ * continuation is RT_EINVAL. */
 #define RT_MULTI_RESERVE_MEAN 1u
 int rt_multi_reserve(rt_multi *m, uint32_t width, uint32_t height, uint32_t band_rows, uint32_t flags);
 
@@ -504,8 +510,19 @@ typedef struct rt_on_render_profile {
     double HostCopyMs;       /* of which: frame -> caller image (CopyImage: DMA [+ host copy]) */
     double HostWaitMs;       /* of which: waiting for an in-flight frame (reset/move) */
     double GpuFrameMs;       /* sum of completed frames' launch -> done GPU time      */
+    uint64_t FrameAllocations; /* frame-buffer (re)allocations by rt_on_init /
+                                  rt_on_render_reserve / a resize beyond them      */
 } rt_on_render_profile;
 int rt_on_render_get_profile(rt_on_render_profile *out, int reset);
+
+/* Sizes the frame driver's device frames (running mean + two RGBA8 frames)
+ * and the trace's launch buffers for images up to width x height, so a later
+ * resize within that size frees and allocates nothing: it re-uses them, as
+ * the reference re-Pushes its images into the arena OnInit sized (main.cpp:
+ * 658, 798-804).  rt_on_init reserves its 1280x720 window (main.cpp:649-650).
+ * Keeps the current frames; on several devices a reservation that grows their
+ * resident means restarts the running mean at the next call.  New. */
+int rt_on_render_reserve(uint32_t width, uint32_t height);
 
 /* ----------------------------------------------------------- output path */
 

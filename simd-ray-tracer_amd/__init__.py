@@ -101,7 +101,8 @@ class RtMultiInfo(ctypes.Structure):  # rt_multi_get_info
 
 class RtOnRenderProfile(ctypes.Structure):  # rt_on_render_get_profile
     _fields_ = [(n, c_uint64) for n in ("Calls", "FramesLaunched", "FramesCopied")] + [
-        (n, c_double) for n in ("CallMs", "HostCopyMs", "HostWaitMs", "GpuFrameMs")]
+        (n, c_double) for n in ("CallMs", "HostCopyMs", "HostWaitMs", "GpuFrameMs")] + [
+        ("FrameAllocations", c_uint64)]
 
 
 RT_MULTI_AUTO, RT_MULTI_RCCL, RT_MULTI_PEER = 0, 1, 2
@@ -166,6 +167,7 @@ SIGNATURES = {
     "rt_on_render_unregister_image": (c_int, []),
     "rt_on_shutdown": (c_int, []),
     "rt_on_render_get_profile": (c_int, [POINTER(RtOnRenderProfile), c_int]),
+    "rt_on_render_reserve": (c_int, [c_uint32, c_uint32]),
     "rt_image_write_ppm": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
     "rt_image_write_png": (c_int, [POINTER(RtImage), c_char_p, c_uint32]),
     "rt_frame_hash": (c_uint64, [c_void_p, c_uint64]),
@@ -572,6 +574,11 @@ def on_render_register_image(image: np.ndarray) -> None:
 
 def on_render_unregister_image() -> None:
     _check(lib().rt_on_render_unregister_image(), "rt_on_render_unregister_image")
+
+
+def on_render_reserve(width: int, height: int) -> None:
+    """rt_on_render_reserve: frames up to width x height need no allocation in the frame loop."""
+    _check(lib().rt_on_render_reserve(width, height), "rt_on_render_reserve")
 
 
 def on_render_wait() -> None:

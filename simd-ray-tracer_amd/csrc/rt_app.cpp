@@ -13,6 +13,8 @@
 // RT_KEY_* bits the caller passes instead of the platform's IsDown().
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
+
+#include <algorithm>
 #include <string.h>
 #include <time.h>
 
@@ -78,6 +80,13 @@ struct App {
     // reference's CopyImage, main.cpp:688-697) while the GPU traces.
     void *d_prev = nullptr;
     uint32_t *d_cur[2] = {nullptr, nullptr};
+    // Pixels the three frame buffers hold (rt_on_render_reserve; OnInit reserves
+    // its window, main.cpp:649-650).  A resize within it reuses them, as the
+    // reference re-Pushes its images into the arena OnInit sized (main.cpp:
+    // 658, 798-804): no call of the frame loop frees or allocates.
+    size_t cap_px = 0;
+    uint32_t reserve_w = 0, reserve_h = 0;  // launch buffers reserved for this geometry (0: none)
+    bool restart_pending = false;  // a reservation dropped the resident mean: the next call restarts it
     uint32_t slot = 0;             // d_cur slot of the last launched frame
     uint64_t *d_rays = nullptr;
     uint64_t *h_rays = nullptr;    // pinned: the last frame's count, copied after its trace
@@ -116,6 +125,55 @@ int wait_frame() {
     const double t = now_ms();
     if (hipEventSynchronize(g_app.ev_done) != hipSuccess) return RT_EIO;
     g_app.prof.HostWaitMs += now_ms() - t;
+    return RT_OK;
+}
+
+// Frame buffers for `px` pixels: grows only beyond the capacity, keeping the
+// running mean and both frames of the current geometry (device copies).
+int ensure_frames(size_t px) {
+    if (px <= g_app.cap_px) return RT_OK;
+    void *prev = nullptr;
+    uint32_t *cur[2] = {nullptr, nullptr};
+    if (hipMalloc(&prev, px * 16u) != hipSuccess || hipMalloc(&cur[0], px * 4u) != hipSuccess ||
+        hipMalloc(&cur[1], px * 4u) != hipSuccess) {
+        (void)hipFree(prev);
+        (void)hipFree(cur[0]);
+        (void)hipFree(cur[1]);
+        return RT_ENOMEM;
+    }
+    const size_t live = (size_t)g_app.width * g_app.height;
+    if (live && g_app.d_prev &&
+        (hipMemcpy(prev, g_app.d_prev, live * 16u, hipMemcpyDeviceToDevice) != hipSuccess ||
+         hipMemcpy(cur[0], g_app.d_cur[0], live * 4u, hipMemcpyDeviceToDevice) != hipSuccess ||
+         hipMemcpy(cur[1], g_app.d_cur[1], live * 4u, hipMemcpyDeviceToDevice) != hipSuccess))
+        return RT_EIO;
+    (void)hipFree(g_app.d_prev);
+    (void)hipFree(g_app.d_cur[0]);
+    (void)hipFree(g_app.d_cur[1]);
+    g_app.d_prev = prev;
+    g_app.d_cur[0] = cur[0];
+    g_app.d_cur[1] = cur[1];
+    g_app.cap_px = px;
+    g_app.prof.FrameAllocations += 1;
+    return RT_OK;
+}
+
+// The trace's launch buffers for a width x height frame (rt_device_reserve, or
+// rt_multi_reserve over the devices' 8-row bands), once per geometry.
+int reserve_launch(uint32_t w, uint32_t h) {
+    if (w <= g_app.reserve_w && h <= g_app.reserve_h) return RT_OK;
+    int rc;
+    if (g_app.multi) {
+        rc = rt_multi_reserve(g_app.multi, w, h, 8u, 0u);
+        // a grown device mean is gone (rt_multi_reserve): restart it next call
+        if (g_app.width && g_app.prev_count) g_app.restart_pending = true;
+    } else {
+        rc = rt_device_reserve(g_app.dev, w, h);
+    }
+    if (rc) return rc;
+    g_app.reserve_w = std::max(g_app.reserve_w, w);
+    g_app.reserve_h = std::max(g_app.reserve_h, h);
+    (void)hipSetDevice(g_app.ordinal);
     return RT_OK;
 }
 
@@ -195,7 +253,21 @@ extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices
         return RT_ENOMEM;
     (void)hipMemset(g_app.d_rays, 0, sizeof(uint64_t));
     g_app.ready = true;
-    return RT_OK;
+    // the window OnInit asks the platform for (main.cpp:649-650): frames up to
+    // that size need no allocation in the frame loop
+    return rt_on_render_reserve(1280u, 720u);
+}
+
+extern "C" int rt_on_render_reserve(uint32_t width, uint32_t height) {
+    DeviceGuard device_guard;  // the caller's current device is restored on return
+    if (!g_app.ready || width == 0 || height == 0 || width > 65536 || height > 65536)
+        return RT_EINVAL;
+    if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
+    const size_t px = (size_t)width * height;
+    if (px <= g_app.cap_px && width <= g_app.reserve_w && height <= g_app.reserve_h) return RT_OK;
+    if (wait_frame() != RT_OK) return RT_EIO;  // growing frees buffers the frame in flight uses
+    if (const int rc = ensure_frames(px)) return rc;
+    return reserve_launch(width, height);
 }
 
 static int on_render(const rt_image *image, rt_render_params params, uint32_t keys, uint64_t *out_total_rays_cast,
@@ -245,19 +317,17 @@ static int on_render(const rt_image *image, rt_render_params params, uint32_t ke
     const bool complete = frame_complete();                                          // :783
     const bool resize = image->Width != g_app.width || image->Height != g_app.height;  // :784
     bool copy_out = complete && !resize;
-    if (resize || moved || (keys & RT_KEY_RESET)) {  // :791-804
+    if (resize || moved || (keys & RT_KEY_RESET) || g_app.restart_pending) {  // :791-804
         if (wait_frame() != RT_OK) return RT_EIO;
         copy_out = !resize;  // the completed frame still goes out (below)
         g_app.prev_count = 0;
+        g_app.restart_pending = false;
         if (resize) {
-            const size_t px = (size_t)image->Width * image->Height;
-            (void)hipFree(g_app.d_prev);
-            (void)hipFree(g_app.d_cur[0]);
-            (void)hipFree(g_app.d_cur[1]);
-            g_app.d_prev = g_app.d_cur[0] = g_app.d_cur[1] = nullptr;
-            if (hipMalloc(&g_app.d_prev, px * 16u) != hipSuccess || hipMalloc(&g_app.d_cur[0], px * 4u) != hipSuccess ||
-                hipMalloc(&g_app.d_cur[1], px * 4u) != hipSuccess)
-                return RT_ENOMEM;
+            // RenderData.Reset + Push (main.cpp:798-804): the reserved buffers are
+            // reused; only a frame beyond the reservation grows them
+            if (const int rc = ensure_frames((size_t)image->Width * image->Height)) return rc;
+            if (const int rc = reserve_launch(image->Width, image->Height)) return rc;
+            g_app.restart_pending = false;  // the resize restarts the mean anyway
             g_app.width = image->Width;
             g_app.height = image->Height;
             g_app.in_flight = false;

@@ -58,6 +58,9 @@ struct rt_device {
     // measured (rtk_launch_pixel_sort), at P >= 4; RT_PIXEL_SORT=0 turns it off.
     // Same box: C2 158.7-159.3k -> 164.6-166.4k Mrays/s, RTWeekend 22.4k -> 23.3k
     int pixel_sort_env = 1;
+    // pixels per dealt unit (TraceArgs.pix_seg): 4-pixel row segments keep each wave's
+    // stores to whole 64-B runs of the v4 image (RT_PIXEL_SEG=1: single pixels)
+    uint32_t pixel_seg = 4;
     int merge_env = -1;  // RT_MERGE_ROUNDS: -1 auto (scenes of at most kMergeGroups groups), 0 never, 1 always
     uint8_t *d_pix_perm = nullptr;  // 64 B per block tile (TraceArgs.pix_perm)
     uint32_t *d_pix_cost = nullptr; // per band pixel (TraceArgs.pix_cost)
@@ -76,9 +79,10 @@ struct rt_device {
     unsigned long long *d_cull_counters = nullptr;  // kCullCounterWords: striped counters + device totals of the cull pass
     uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
     size_t tile_cap = 0, mask_cap = 0;
-    // rt_device_reserve: the geometry the launch buffers are pre-sized for (0: none);
-    // a scene upload re-applies it for the new scene's mask words
-    uint32_t reserve_width = 0, reserve_rows = 0;
+    // rt_device_reserve: the most block tiles (over every lanes-per-pixel shape)
+    // and band pixels of any geometry reserved so far (0: none)
+    uint32_t reserve_tiles = 0;
+    size_t reserve_pixels = 0;
     size_t mask_words = 0;  // words the last cull pass wrote (rt_debug_masks)
     // the launch (camera, scene, geometry) the masks / live list / order were made for
     std::vector<uint32_t> tile_key;
@@ -208,6 +212,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (mr && (mr[0] == '0' || mr[0] == '1')) d->merge_env = mr[0] - '0';
     const char *psort = getenv("RT_PIXEL_SORT");
     if (psort && (psort[0] == '0' || psort[0] == '1')) d->pixel_sort_env = psort[0] - '0';
+    const char *pseg = getenv("RT_PIXEL_SEG");
+    if (pseg && (pseg[0] == '1' || pseg[0] == '2' || pseg[0] == '4')) d->pixel_seg = (uint32_t)(pseg[0] - '0');
     const char *ppl = getenv("RT_PIXELS_PER_LANE");
     if (ppl && (ppl[0] == '1' || ppl[0] == '4')) d->pixels_per_lane_env = ppl[0] - '0';
     const char *st = getenv("RT_STATS");
@@ -880,8 +886,15 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     d->scene_set = true;
     d->scene_gen += 1;
     // a reserved geometry keeps its promise for the new scene's mask words (the
-    // device is quiescent here: the upload waited for every launch)
-    return apply_reserve(d);
+    // device is quiescent here: the upload waited for every launch).  The scene
+    // is committed by now, so a failure here does not fail the upload: the
+    // reservation is dropped and later launches grow their buffers lazily.
+    if (apply_reserve(d) != RT_OK) {
+        (void)hipGetLastError();
+        d->reserve_tiles = 0;
+        d->reserve_pixels = 0;
+    }
+    return RT_OK;
 }
 
 extern "C" int rt_scene_prefilter(const rt_scene *scene, uint32_t enable_simd, float *out_r2, float *out_r2p,
@@ -999,16 +1012,14 @@ static int ensure_pixel_sort(rt_device *d, uint32_t n_tiles, size_t pixels, hipS
 // the most block tiles over every lanes-per-pixel shape (rt_trace picks P per
 // launch) and the current scene's mask words, so no later launch allocates.
 static int apply_reserve(rt_device *d) {
-    if (!d->reserve_width) return RT_OK;
-    uint32_t n_tiles = 0;
-    for (const int p : {1, 2, 4, 8, 16, 32})
-        n_tiles = std::max(n_tiles, rtk_tile_count(d->reserve_width, d->reserve_rows, p));
+    if (!d->reserve_tiles) return RT_OK;
+    const uint32_t n_tiles = d->reserve_tiles;
     uint32_t n_words = 1;
     if (d->scene_set)
         for (int rs = 0; rs < 2; ++rs) n_words = std::max(n_words, (d->n_groups[rs] + 63u) / 64u);
     if (const int rc = ensure_tile_buffers(d, n_tiles, nullptr, true)) return rc;
     if (d->pixel_sort_env)
-        if (const int rc = ensure_pixel_sort(d, n_tiles, (size_t)d->reserve_width * d->reserve_rows, nullptr, true))
+        if (const int rc = ensure_pixel_sort(d, n_tiles, d->reserve_pixels, nullptr, true))
             return rc;
     return ensure_masks(d, (size_t)n_tiles * 4u * n_words, nullptr, true);
 }
@@ -1018,8 +1029,10 @@ extern "C" int rt_device_reserve(rt_device *d, uint32_t width, uint32_t local_ro
     if (!d || width == 0 || local_rows == 0 || width > 65536 || local_rows > 65536)
         return fail(RT_EINVAL, "rt_device_reserve: bad argument");
     HIP_OK(hipSetDevice(d->ordinal));
-    d->reserve_width = std::max(d->reserve_width, width);
-    d->reserve_rows = std::max(d->reserve_rows, local_rows);
+    uint32_t n_tiles = 0;
+    for (const int p : {1, 2, 4, 8, 16, 32}) n_tiles = std::max(n_tiles, rtk_tile_count(width, local_rows, p));
+    d->reserve_tiles = std::max(d->reserve_tiles, n_tiles);
+    d->reserve_pixels = std::max(d->reserve_pixels, (size_t)width * local_rows);
     return apply_reserve(d);
 }
 
@@ -1268,6 +1281,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.tile_order = d->tile_order_valid ? d->d_tile_order : nullptr;
     a.tile_cost = sched ? d->d_tile_cost : nullptr;
     a.pix_perm = pixel_sort ? d->d_pix_perm : nullptr;
+    a.pix_seg = d->pixel_seg;
     d->last.PixelsSorted = pixel_sort && !new_key && d->n_sorts > 0 ? 1u : 0u;
     d->last_n_tiles = n_tiles;
     d->last_frames = desc->Frames;

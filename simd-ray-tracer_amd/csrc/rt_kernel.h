@@ -95,6 +95,11 @@ struct TraceArgs {
     // sphere loop (scenes of at most kMergeGroups groups: the cull mask and the prefilter
     // save nothing there, and split rounds leave most lanes idle at one frame per launch)
     uint32_t merge_rounds;
+    // pixels per dealt unit of the pixel sort (1, 2 or 4; capped at the wave's pixel count): the
+    // sort ranks row segments of pix_seg pixels by their summed cost, so each wave's owner
+    // lanes store whole 4-pixel runs (a 64-B half line of the v4 image) instead of single
+    // pixels of lines other waves -- on other XCDs -- also write
+    uint32_t pix_seg;
 };
 constexpr uint32_t kMergeGroups = 2;
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)

@@ -1766,6 +1766,8 @@ __global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t 
 #ifndef RTK_P16_TU  // (the P = 16 translation unit holds only its trace launches: see launch_p16)
 // One wave per block tile: rank its pixels by the last launch's cost (ties by
 // index), so wave w of the next launch gets ranks [NPIX w, NPIX (w + 1)).
+// With pix_seg = S > 1 the ranked units are row segments of S pixels (summed
+// cost), dealt whole: a wave's pixels then form S-pixel runs of a row.
 template <int P>
 __global__ __launch_bounds__(64) void pixel_sort_kernel(TraceArgs a, uint8_t *perm) {
     constexpr uint32_t TW = Shape<P>::TW, TH = Shape<P>::TH, BW = 2u * TW, NB = 4u * TW * TH;
@@ -1788,12 +1790,17 @@ __global__ __launch_bounds__(64) void pixel_sort_kernel(TraceArgs a, uint8_t *pe
         const uint32_t x = tile_x * BW + lane % BW, ly = tile_y * (2u * TH) + lane / BW;
         c = x < a.width && ly < a.local_rows ? a.pix_cost[(size_t)ly * a.width + x] : 0u;
     }
+    // segment size: a power of two dividing the block row (BW) and the wave's pixels
+    constexpr uint32_t NPIX = NB / 4u;
+    const uint32_t S = a.pix_seg >= 4u && NPIX >= 4u && BW % 4u == 0 ? 4u : a.pix_seg >= 2u && NPIX >= 2u ? 2u : 1u;
+    for (uint32_t off = 1; off < S; off <<= 1) c += (uint32_t)__shfl_xor((int)c, (int)off, 64);  // (every lane active)
+    const uint32_t seg = lane / S, nseg = NB / S;
     uint32_t rank = 0;
-    for (uint32_t i = 0; i < NB; ++i) {
-        const uint32_t ci = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)i);
-        rank += ci < c || (ci == c && i < lane) ? 1u : 0u;
+    for (uint32_t i = 0; i < nseg; ++i) {
+        const uint32_t ci = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)(i * S));
+        rank += ci < c || (ci == c && i < seg) ? 1u : 0u;
     }
-    if (lane < NB) pp[rank] = (uint8_t)lane;
+    if (lane < NB) pp[rank * S + lane % S] = (uint8_t)lane;
 }
 
 // Scatter RCCL-gathered compact band images into the full framebuffer.

@@ -357,6 +357,9 @@ extern "C" int rt_multi_reserve(rt_multi *m, uint32_t width, uint32_t height, ui
     const uint32_t maxr = max_local_rows(height, R, n);
     for (Shard &sh : m->s) {
         MHIP(hipSetDevice(sh.ordinal));
+        // growing a shard's resident running mean discards it (grow() does not
+        // copy), so no continuation may blend onto the new buffer
+        if ((size_t)maxr * width * 16u > sh.cap_prev) m->accum_valid = false;
         if (const int rc = grow(&sh.prev, &sh.cap_prev, (size_t)maxr * width * 16u)) return rc;
         size_t cap = sh.cap_cur;
         for (int b = 0; b < kSlots; ++b) {

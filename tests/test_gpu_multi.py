@@ -313,3 +313,29 @@ def test_multi_reserve_means_no_allocation_in_later_calls(rt, orc, torch_cuda):
         assert m.last_gather_ms() >= 0.0
     finally:
         m.close()
+
+
+def test_multi_reserve_that_grows_the_mean_refuses_a_continuation(rt, orc, torch_cuda):
+    """rt_multi_reserve growing the devices' resident running means discards
+    them: after trace (geometry G) + reserve (larger) a continuation at G is
+    RT_EINVAL instead of blending onto uninitialised memory, and a restart then
+    continues bit-exactly (the oracle's frame)."""
+    torch = torch_cuda
+    s = rt.scene_prefix(rt.scene_builtin(1), 16)
+    W, H, B = 64, 48, 6
+    cam = rt.camera_setup(s, W, H)
+    m = rt.Multi([0, 0])
+    try:
+        m.upload_scene(s)
+        multi_render(rt, torch, m, cam, W, H, 2, B, prev_count=0, accum_zero=True)
+        m.reserve(4 * W, 4 * H, 8)
+        with pytest.raises(rt.RtError, match="no resident running mean"):
+            multi_render(rt, torch, m, cam, W, H, 1, B, prev_count=2)
+        multi_render(rt, torch, m, cam, W, H, 2, B, prev_count=0, accum_zero=True)
+        got = multi_render(rt, torch, m, cam, W, H, 1, B, prev_count=2)
+    finally:
+        m.close()
+    o = orc.scene_builtin(1).prefix(16)
+    oprev, ocur, _ = orc.render(o, orc.camera(o, W, H), W, H, frames=3, max_bounce=B)
+    assert np.array_equal(got[0].cpu().numpy().view(np.uint32).reshape(-1, 4), oprev.view(np.uint32))
+    assert np.array_equal(got[1].cpu().numpy().view(np.uint32), ocur)

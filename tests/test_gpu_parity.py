@@ -806,3 +806,88 @@ def test_first_launch_split_changes_no_bit(rt, orc, torch_cuda, monkeypatch, sim
             r = orc.render(o, oc, W, H, frames=S, max_bounce=B, simd=simd, threads=orc.cpu_threads(),
                            prev_count=pc, prev=base[0])
         assert_same(*out[1], *r)
+
+
+def test_on_render_resize_returns_no_frame_and_restarts_at_the_new_size(rt, orc, torch_cuda):
+    """A call with a different-size image (main.cpp:784-804): it waits for the
+    frame in flight, returns 0 and leaves the image alone (CopyToOutput is
+    false), restarts the mean, and the next completed frame is frame 0 at the
+    new size -- every later one the mean over one more frame.  Within the
+    reservation (rt_on_init's 1280x720 window, then rt_on_render_reserve) no
+    resize allocates frame buffers."""
+    rt.on_init()
+    try:
+        o = orc.scene_builtin(1)
+        allocs0 = rt.on_render_profile()["FrameAllocations"]
+        sizes = [(48, 40), (64, 32), (33, 70), (64, 32)]
+        for i, (W, H) in enumerate(sizes):
+            img = np.full((H, W), 0xDEADBEEF, np.uint32)
+            done, rays, _ = rt.on_render(img, 1)  # resize (first call: from no image at all)
+            assert not done and rays == 0
+            assert np.all(img == 0xDEADBEEF), "a resize must not write the image"
+            ocam = orc.camera(o, W, H)
+            for k in range(3):
+                if i != 1:  # size 1: busy-poll without waiting, like a platform loop
+                    rt.on_render_wait()
+                while True:
+                    done, rays, _ = rt.on_render(img, 1)
+                    if done:
+                        break
+                _, ocur, orays = orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5)
+                assert np.array_equal(img.reshape(-1), ocur), (W, H, k)
+                assert rays == orc.render(o, ocam, W, H, prev_count=k, frames=1, max_bounce=5)[2], (W, H, k)
+        # the mid-loop resize in flight: no wait before it
+        W, H = sizes[0]
+        img = np.zeros((H, W), np.uint32)
+        assert not rt.on_render(img, 1)[0]
+        assert rt.on_render_profile()["FrameAllocations"] == allocs0, "a resize within the reservation allocated"
+        # beyond the reservation: reserve first, then resize without allocation
+        rt.on_render_reserve(1600, 900)
+        allocs1 = rt.on_render_profile()["FrameAllocations"]
+        assert allocs1 == allocs0 + 1
+        for W, H in ((1600, 900), (1500, 800), (96, 64)):
+            img = np.zeros((H, W), np.uint32)
+            rt.on_render_wait()
+            assert not rt.on_render(img, 1)[0]
+        rt.on_render_wait()
+        assert rt.on_render(img, 1)[0]
+        _, ocur, _ = orc.render(o, orc.camera(o, 96, 64), 96, 64, frames=1, max_bounce=5)
+        assert np.array_equal(img.reshape(-1), ocur)
+        assert rt.on_render_profile()["FrameAllocations"] == allocs1
+        rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
+
+
+def test_on_render_reset_key_hands_out_the_completed_frame_and_restarts(rt, orc, torch_cuda):
+    """R (main.cpp:791-806): the call waits for the frame in flight, copies the
+    COMPLETED frame out (returns 1 with that frame), and restarts the mean: the
+    next frame handed out is frame 0 again.  Both rule sets; once with the
+    frame still in flight at the R call."""
+    rt.on_init()
+    try:
+        W, H = 56, 40
+        o = orc.scene_builtin(0)
+        ocam = orc.camera(o, W, H)
+        want = [orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5)[1] for k in range(4)]
+        want_scalar = [orc.render(o, ocam, W, H, frames=k + 1, max_bounce=5, simd=False)[1] for k in range(4)]
+        img = np.zeros((H, W), np.uint32)
+        for simd, ref in ((True, want), (False, want_scalar)):
+            rt.on_render(img, 0, simd, keys=rt.KEY_RESET)  # restart under these rules
+            for k in range(3):
+                rt.on_render_wait()
+                assert rt.on_render(img, 0, simd)[0]
+                assert np.array_equal(img.reshape(-1), ref[k]), (simd, k)
+            # R while frame 3 may still be in flight: waits, hands out the 4-frame mean
+            done, rays, _ = rt.on_render(img, 0, simd, keys=rt.KEY_RESET)
+            assert done
+            assert np.array_equal(img.reshape(-1), ref[3]), simd
+            rt.on_render_wait()
+            assert rt.on_render(img, 0, simd)[0]
+            assert np.array_equal(img.reshape(-1), ref[0]), simd  # the mean restarted
+            rt.on_render_wait()
+            assert rt.on_render(img, 0, simd)[0]
+            assert np.array_equal(img.reshape(-1), ref[1]), simd
+        rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
