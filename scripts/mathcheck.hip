@@ -21,13 +21,25 @@ __device__ __forceinline__ float sqrt_fast(float x) {
     if (__builtin_fmaf(-sp, s, x) > 0.0f) r = sp;
     return r;
 }
+__device__ __forceinline__ float sqrt_down(float x) {  // the residual fix toward zero only
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    return __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+}
+__device__ __forceinline__ float sqrt_up(float x) {  // the residual fix away from zero only
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    return __builtin_fmaf(-sp, s, x) > 0.0f ? sp : s;
+}
 __device__ __forceinline__ float div_fast(float a, float b, float y) {
     const float q0 = a * y;
     const float r = __builtin_fmaf(-q0, b, a);
     return __builtin_fmaf(r, y, q0);
 }
 
+__device__ unsigned long long g_hist[256];  // mismatches per biased exponent of the input (unary modes)
 __device__ void report(unsigned long long *cnt, uint32_t *bad, uint32_t a, uint32_t b) {
+    atomicAdd(&g_hist[(a >> 23) & 0xFFu], 1ull);
     const unsigned long long i = atomicAdd(cnt, 1ull);
     if (i < 8) { bad[2 * i] = a; bad[2 * i + 1] = b; }
 }
@@ -40,7 +52,11 @@ __global__ void k_unary(int mode, int e0, unsigned long long *cnt, uint32_t *bad
     const float x = __uint_as_float(u);
     float got, want;
     if (mode == 0) { got = rcp_fast(x); want = 1.0f / x; }
-    else { got = sqrt_fast(x); want = __builtin_sqrtf(x); }
+    else if (mode == 1) { got = sqrt_fast(x); want = __builtin_sqrtf(x); }
+    else if (mode == 2) { got = __builtin_amdgcn_sqrtf(x); want = __builtin_sqrtf(x); }   // raw v_sqrt_f32
+    else if (mode == 3) { got = sqrt_down(x); want = __builtin_sqrtf(x); }               // only the -1ulp fix
+    else if (mode == 4) { got = sqrt_up(x); want = __builtin_sqrtf(x); }                 // only the +1ulp fix
+    else { got = __builtin_amdgcn_rcpf(x); want = 1.0f / x; }                            // raw v_rcp_f32
     if (__float_as_uint(got) != __float_as_uint(want)) report(cnt, bad, u, 0);
 }
 
@@ -80,6 +96,7 @@ int main() {
     uint32_t *bad;
     (void)hipMalloc(&cnt, 8);
     (void)hipMalloc(&bad, 64);
+    bool hist = true;
     auto run = [&](const char *name, auto launch) {
         (void)hipMemset(cnt, 0, 8);
         (void)hipMemset(bad, 0, 64);
@@ -92,10 +109,25 @@ int main() {
         printf("%-34s mismatches %llu", name, c);
         for (int i = 0; i < 8 && i < (int)c; ++i) printf("  [%08x %08x]", h[2 * i], h[2 * i + 1]);
         printf("\n");
+        unsigned long long hh[256];
+        (void)hipMemcpyFromSymbol(hh, HIP_SYMBOL(g_hist), sizeof(hh));
+        if (c && hist) {  // where the mismatches lie (x in [2^(e-127), 2^(e-126)))
+            printf("    by input exponent:");
+            for (int e = 0; e < 256; ++e)
+                if (hh[e]) printf(" 2^%d:%llu", e - 127, hh[e]);
+            printf("\n");
+        }
+        unsigned long long z[256] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_hist), z, sizeof(z));
     };
     // exponents 127-40 .. 127+40: x in [2^-40, 2^40)
     run("rcp  rcp+Newton, 2^-40..2^40", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 80), dim3(256), 0, 0, 0, 87, cnt, bad); });
     run("sqrt v_sqrt+fix, 2^-60..2^60", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 1, 67, cnt, bad); });
+    // is either fix-up step ever needed? (raw instructions and one-sided fixes, same range)
+    run("sqrt raw v_sqrt_f32, 2^-60..2^60", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 2, 67, cnt, bad); });
+    run("sqrt v_sqrt + down fix only", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 3, 67, cnt, bad); });
+    run("sqrt v_sqrt + up fix only", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 4, 67, cnt, bad); });
+    run("rcp  raw v_rcp_f32, 2^-40..2^40", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 80), dim3(256), 0, 0, 5, 87, cnt, bad); });
     // b in [2^-8, 2^8), a in [2^-40, 2^24): quotients 2^-48 .. 2^32 (normal)
     for (int rep = 0; rep < 4; ++rep)
         run("div  q0+fma, b 2^-8..2^8", [&] { hipLaunchKernelGGL(k_div, dim3(16384), dim3(256), 0, 0, 0x1234567ull + rep, 512, 87, 119, cnt, bad); });

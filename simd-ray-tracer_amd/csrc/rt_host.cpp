@@ -58,9 +58,11 @@ struct rt_device {
     // measured (rtk_launch_pixel_sort), at P >= 4; RT_PIXEL_SORT=0 turns it off.
     // Same box: C2 158.7-159.3k -> 164.6-166.4k Mrays/s, RTWeekend 22.4k -> 23.3k
     int pixel_sort_env = 1;
-    // pixels per dealt unit (TraceArgs.pix_seg): 4-pixel row segments keep each wave's
-    // stores to whole 64-B runs of the v4 image (RT_PIXEL_SEG=1: single pixels)
-    uint32_t pixel_seg = 4;
+    // pixels per dealt unit (TraceArgs.pix_seg), RT_PIXEL_SEG=1/2/4: 4-pixel row segments keep
+    // each wave's stores to whole 64-B runs of the v4 image (HBM writes per launch: C2 20.9 ->
+    // 17.5 MB, RTWeekend 80.2 -> 57.3 MB) but deal costs coarser: C2 -2.2 %, RTWeekend -4 %
+    // (profiles/r05b_pixel_seg_ab.txt), so single pixels stay the default
+    uint32_t pixel_seg = 1;
     int merge_env = -1;  // RT_MERGE_ROUNDS: -1 auto (scenes of at most kMergeGroups groups), 0 never, 1 always
     uint8_t *d_pix_perm = nullptr;  // 64 B per block tile (TraceArgs.pix_perm)
     uint32_t *d_pix_cost = nullptr; // per band pixel (TraceArgs.pix_cost)

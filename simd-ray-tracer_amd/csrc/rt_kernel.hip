@@ -80,11 +80,17 @@ __device__ __forceinline__ float rcp_rn(float b) {
 // RN(sqrt(x)) for x = 0 or x in [2^-60, 2^60]: v_sqrt_f32 (< 1 ulp) and
 // the +-1 ulp residual test (the compiler's sequence minus its
 // denormal/infinity range scaling).
+// RTK_SQRT_FIX (experiment builds only, scripts/mathcheck.hip decides): 2 = both
+// residual tests, 1 = the -1 ulp test only, 3 = the +1 ulp test only, 0 = none.
+#ifndef RTK_SQRT_FIX
+#define RTK_SQRT_FIX 2
+#endif
 __device__ __forceinline__ float sqrt_rn(float x) {
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
-    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+    float r = s;
+    if (RTK_SQRT_FIX == 1 || RTK_SQRT_FIX == 2) r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    if (RTK_SQRT_FIX == 2 || RTK_SQRT_FIX == 3) r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
     return r;
 }
 
@@ -139,13 +145,18 @@ struct Lut {
     bool in_lds;  // wave-uniform
 };
 
+// For a positive normal v with unbiased exponent e: the entry is
+// (e & 1) * 1024 + mantissa[22:13], i.e. bits [23:13] of v with bit 23 (the
+// biased exponent's parity, the opposite of e's) flipped; the scale is
+// floor(e / 2), which is (int)(bits(v) - bits(1.0f)) >> 24 (the mantissa adds
+// less than half a unit of that shift).  Checked against the direct form on
+// every positive normal f32 (index and result bits): two bit-field ops instead
+// of five, most of them the half-rate shift class.
 __device__ __forceinline__ float rsqrt_x86(const Lut &lut, float v) {
     const uint32_t u = __float_as_uint(v);
-    const int32_t e = (int32_t)((u >> 23) & 0xFFu) - 127;
-    const uint32_t par = (uint32_t)e & 1u;
-    const uint32_t idx = par * 1024u + ((u >> 13) & 1023u);
+    const uint32_t idx = ((u >> 13) & 2047u) ^ 1024u;
     const float base = lut.in_lds ? lut.lds[idx] : lut.glob[idx];
-    const int32_t sh = (e - (int32_t)par) >> 1;
+    const int32_t sh = (int32_t)(u - 0x3F800000u) >> 24;
     return __uint_as_float(__float_as_uint(base) - ((uint32_t)sh << 23));
 }
 
