@@ -63,6 +63,10 @@ struct rt_device {
     // 17.5 MB, RTWeekend 80.2 -> 57.3 MB) but deal costs coarser: C2 -2.2 %, RTWeekend -4 %
     // (profiles/r05b_pixel_seg_ab.txt), so single pixels stay the default
     uint32_t pixel_seg = 1;
+    // RGBA8 encoded from the running mean by a coalesced pass after the launch (TraceArgs.skip_cur),
+    // at P >= 2: trace-kernel HBM writes C2 21.0 -> 15.7 MB, RTWeekend 80.6 -> 54.1 MB, C2 +0.7 %
+    // (profiles/r05e_cur_pass_ab.txt); RT_CUR_PASS=0 stores RGBA8 in the trace kernel
+    uint32_t cur_pass = 1;
     int merge_env = -1;  // RT_MERGE_ROUNDS: -1 auto (scenes of at most kMergeGroups groups), 0 never, 1 always
     uint8_t *d_pix_perm = nullptr;  // 64 B per block tile (TraceArgs.pix_perm)
     uint32_t *d_pix_cost = nullptr; // per band pixel (TraceArgs.pix_cost)
@@ -214,6 +218,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (mr && (mr[0] == '0' || mr[0] == '1')) d->merge_env = mr[0] - '0';
     const char *psort = getenv("RT_PIXEL_SORT");
     if (psort && (psort[0] == '0' || psort[0] == '1')) d->pixel_sort_env = psort[0] - '0';
+    const char *cps = getenv("RT_CUR_PASS");
+    if (cps && (cps[0] == '0' || cps[0] == '1')) d->cur_pass = (uint32_t)(cps[0] - '0');
     const char *pseg = getenv("RT_PIXEL_SEG");
     if (pseg && (pseg[0] == '1' || pseg[0] == '2' || pseg[0] == '4')) d->pixel_seg = (uint32_t)(pseg[0] - '0');
     const char *ppl = getenv("RT_PIXELS_PER_LANE");
@@ -1284,6 +1290,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.tile_cost = sched ? d->d_tile_cost : nullptr;
     a.pix_perm = pixel_sort ? d->d_pix_perm : nullptr;
     a.pix_seg = d->pixel_seg;
+    // (multi-frame launches only: a one-frame launch, OnRender's, keeps its store and one kernel fewer)
+    a.skip_cur = d->cur_pass && lpp >= 2 ? 1u : 0u;
     d->last.PixelsSorted = pixel_sort && !new_key && d->n_sorts > 0 ? 1u : 0u;
     d->last_n_tiles = n_tiles;
     d->last_frames = desc->Frames;
@@ -1328,6 +1336,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             d->tile_order_valid = true;
         }
     }
+    // RT_CUR_PASS: the RGBA8 band image from the running mean the kernels stored (main.cpp:490's
+    // store on its own, the same bits), written by one coalesced pass
+    if (a.skip_cur && desc->Frames > 0 &&
+        rtk_launch_encode(a.prev, a.cur, (uint64_t)local_rows * desc->Width, (a.flags & kFlagSrgbPow) ? 1u : 0u, s) != 0)
+        return fail(RT_EIO, "rt_trace: RGBA8 encode launch failed: %s", hipGetErrorString(hipGetLastError()));
     d->last.SplitHeadFrames = head_frames;
     return RT_OK;
 }

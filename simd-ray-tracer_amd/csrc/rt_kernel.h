@@ -100,6 +100,10 @@ struct TraceArgs {
     // lanes store whole 4-pixel runs (a 64-B half line of the v4 image) instead of single
     // pixels of lines other waves -- on other XCDs -- also write
     uint32_t pix_seg;
+    // 1: the trace and empty-tile kernels store only the running mean; the RGBA8 image is
+    // encoded from it by one coalesced pass after the launch (rtk_launch_encode), so its 4-B
+    // pixels are not written as scattered partial lines from several XCDs (RT_CUR_PASS)
+    uint32_t skip_cur;
 };
 constexpr uint32_t kMergeGroups = 2;
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)

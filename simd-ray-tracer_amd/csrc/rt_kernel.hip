@@ -1149,7 +1149,7 @@ void trace_kernel(TraceArgs a) {
     auto store_pixel = [&]() {
         const size_t pix = (size_t)ly * a.width + x;
         a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
-        a.cur[pix] = rgba8(accx, accy, accz, Q == 1 && (a.flags & kFlagSrgbPow) != 0u);
+        if (!a.skip_cur) a.cur[pix] = rgba8(accx, accy, accz, Q == 1 && (a.flags & kFlagSrgbPow) != 0u);
     };
 
     // owner lanes of in-image pixels (they fold until every frame is folded)
@@ -1771,7 +1771,7 @@ __global__ __launch_bounds__(256) void empty_kernel(TraceArgs a, const uint32_t 
         }
     }
     a.prev[pix] = make_float4(accx, accy, accz, 1.0f);
-    a.cur[pix] = rgba8(accx, accy, accz, (a.flags & kFlagSrgbPow) != 0u);
+    if (!a.skip_cur) a.cur[pix] = rgba8(accx, accy, accz, (a.flags & kFlagSrgbPow) != 0u);
 }
 
 #ifndef RTK_P16_TU  // (the P = 16 translation unit holds only its trace launches: see launch_p16)
