@@ -63,6 +63,9 @@ struct rt_device {
     // 17.5 MB, RTWeekend 80.2 -> 57.3 MB) but deal costs coarser: C2 -2.2 %, RTWeekend -4 %
     // (profiles/r05b_pixel_seg_ab.txt), so single pixels stay the default
     uint32_t pixel_seg = 1;
+    // RT_XCD_GROUP: every wave of a block tile on one XCD (rtk_launch_xcd_group), so its lines'
+    // partial stores merge in one L2 before they are written back
+    int xcd_group_env = 1;
     // RGBA8 encoded from the running mean by a coalesced pass after the launch (TraceArgs.skip_cur),
     // at P >= 2: trace-kernel HBM writes C2 21.0 -> 15.7 MB, RTWeekend 80.6 -> 54.1 MB, C2 +0.7 %
     // (profiles/r05e_cur_pass_ab.txt); RT_CUR_PASS=0 stores RGBA8 in the trace kernel
@@ -81,6 +84,7 @@ struct rt_device {
     uint32_t split_growth = 3;        // each leading part this many times the previous (RT_SPLIT_GROWTH)
     uint32_t order_launches = 6;      // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept
     uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
+    uint32_t *d_tile_order_sorted = nullptr;  // the sort's output before XCD grouping (rtk_launch_xcd_group)
     uint32_t *d_tile_live = nullptr;
     unsigned long long *d_cull_counters = nullptr;  // kCullCounterWords: striped counters + device totals of the cull pass
     uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
@@ -220,6 +224,8 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (psort && (psort[0] == '0' || psort[0] == '1')) d->pixel_sort_env = psort[0] - '0';
     const char *cps = getenv("RT_CUR_PASS");
     if (cps && (cps[0] == '0' || cps[0] == '1')) d->cur_pass = (uint32_t)(cps[0] - '0');
+    const char *xg = getenv("RT_XCD_GROUP");
+    if (xg && (xg[0] == '0' || xg[0] == '1')) d->xcd_group_env = xg[0] - '0';
     const char *pseg = getenv("RT_PIXEL_SEG");
     if (pseg && (pseg[0] == '1' || pseg[0] == '2' || pseg[0] == '4')) d->pixel_seg = (uint32_t)(pseg[0] - '0');
     const char *ppl = getenv("RT_PIXELS_PER_LANE");
@@ -247,6 +253,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_wave_times);
     (void)hipFree(d->d_tile_cost);
     (void)hipFree(d->d_tile_order);
+    (void)hipFree(d->d_tile_order_sorted);
     (void)hipFree(d->d_tile_scratch);
     (void)hipFree(d->d_tile_live);
     (void)hipFree(d->d_cull_counters);
@@ -959,7 +966,8 @@ static int ensure_tile_buffers(rt_device *d, uint32_t n_tiles, hipStream_t sync,
     if (device_wide) HIP_OK(hipDeviceSynchronize());
     else HIP_OK(hipStreamSynchronize(sync));
     if (n_tiles > d->tile_cap) {
-        for (uint32_t **b : {&d->d_tile_cost, &d->d_tile_order, &d->d_tile_scratch, &d->d_tile_live}) {
+        for (uint32_t **b : {&d->d_tile_cost, &d->d_tile_order, &d->d_tile_scratch, &d->d_tile_live,
+                             &d->d_tile_order_sorted}) {
             (void)hipFree(*b);
             *b = nullptr;
         }
@@ -967,6 +975,7 @@ static int ensure_tile_buffers(rt_device *d, uint32_t n_tiles, hipStream_t sync,
         // cost / order / sort scratch per unit: up to 4 per block tile (wave units)
         if (hipMalloc(&d->d_tile_cost, 4u * n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_order, 4u * n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_order_sorted, 4u * n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(4u * n_tiles)) != hipSuccess)
             return fail(RT_ENOMEM, "rt_trace: tile order buffers");
@@ -1319,6 +1328,10 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         done_frames += split[part];
         const bool resort = sched && any_live && (d->n_sorts < d->order_launches || part + 1 < n_split);
         a.pix_cost = pixel_sort && resort ? d->d_pix_cost : nullptr;
+        // wave costs only for a launch whose costs are sorted: once the order is kept, the
+        // per-wave 4-B cost stores (scattered partial lines, ~8 MB of HBM writes per 1080p
+        // launch at P = 4) would feed nothing
+        a.tile_cost = resort ? d->d_tile_cost : nullptr;
         if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, grid_tiles, s) != 0)
             return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         if (any_dead && rtk_launch_empty(&a, lpp, d->d_tile_live, d->d_cull_counters + kCullTotals + 1, s) != 0)
@@ -1329,7 +1342,12 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         // of an 8-rank C2 share) are skipped
         if (resort) {
             d->n_sorts += 1;
-            if (rtk_launch_tile_sort(d->d_tile_cost, d->d_tile_order, d->d_tile_scratch, n_units, s) != 0)
+            // one-wave kernels: sort, then group each block tile's waves onto one XCD
+            const bool group = a.unit_waves && d->xcd_group_env;
+            if (rtk_launch_tile_sort(d->d_tile_cost, group ? d->d_tile_order_sorted : d->d_tile_order,
+                                     d->d_tile_scratch, n_units, s) != 0 ||
+                (group && rtk_launch_xcd_group(d->d_tile_order_sorted, d->d_tile_order, n_units,
+                                               d->d_cull_counters + kCullTotals, d->d_tile_scratch, s) != 0))
                 return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
             if (pixel_sort && rtk_launch_pixel_sort(&a, lpp, d->d_pix_perm, s) != 0)
                 return fail(RT_EIO, "rt_trace: pixel sort launch failed: %s", hipGetErrorString(hipGetLastError()));

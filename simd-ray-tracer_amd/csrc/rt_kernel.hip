@@ -1958,6 +1958,93 @@ __global__ __launch_bounds__(kSortBlock) void tile_rank_kernel(uint32_t *cost, u
     }
 }
 
+// ---- XCD grouping of the wave order (one-wave kernels).  Workgroups are dealt
+// round-robin to the 8 XCDs (block b and b + 8 share one; MI355X_MICROARCH.md,
+// "Workgroup dispatch"), so the four waves of a block tile, which store
+// neighbouring pixels of the same 128-B lines, land on up to four XCDs whose
+// L2s each write their part of every line back (the excess HBM writes of §4).
+// Grouping keeps the per-wave heaviest-first order but moves every unit of block
+// tile t into XCD group x = t & 7: the live prefix [0, L) of the sorted order is
+// partitioned stably by x (each group stays heaviest first), and group x's r-th
+// unit goes to position 8r + x while r < m (the smallest group's size), so block
+// 8r + x runs on the group's XCD; the r >= m leftovers (the lightest units of the
+// larger groups) follow at 8m + ..., group by group.  A permutation of [0, L):
+// no unit is lost or repeated; [L, n) (dead tiles' units) is copied as is.
+constexpr uint32_t kXgBlock = 1024, kXgWaves = kXgBlock / 64;
+
+__device__ __forceinline__ uint32_t xg_group(const uint32_t *in, uint32_t i, uint32_t live_units) {
+    return i < live_units ? (in[i] >> 2) & 7u : 8u;
+}
+
+__global__ __launch_bounds__(kXgBlock) void xg_count_kernel(const uint32_t *in, uint32_t n,
+                                                            const unsigned long long *live_tiles, uint32_t *bc) {
+    __shared__ uint32_t wc[kXgWaves][8];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, i = blockIdx.x * kXgBlock + threadIdx.x;
+    const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
+    const uint32_t x = xg_group(in, i, L);
+    for (uint32_t v = 0; v < 8u; ++v) {
+        const uint64_t m = __ballot(x == v);
+        if (lane == v) wc[wave][v] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8u) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kXgWaves; ++w) t += wc[w][threadIdx.x];
+        bc[8u * blockIdx.x + threadIdx.x] = t;
+    }
+}
+
+// one wave: per-group exclusive scan over the blocks (in place), then the group
+// sizes c_x, m = min c_x and the leftover bases at bc[8 n_blk ..]
+__global__ __launch_bounds__(64) void xg_scan_kernel(uint32_t *bc, uint32_t n_blk) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t run = 0;
+    if (lane < 8u)
+        for (uint32_t b = 0; b < n_blk; ++b) {
+            const uint32_t c = bc[8u * b + lane];
+            bc[8u * b + lane] = run;
+            run += c;
+        }
+    uint32_t m = lane < 8u ? run : 0xFFFFFFFFu;
+    for (int off = 1; off < 8; off <<= 1) m = min(m, (uint32_t)__shfl_xor((int)m, off, 64));
+    m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+    // base_x = sum over y < x of (c_y - m)
+    uint32_t extra = lane < 8u ? run - m : 0u, base = 0;
+    for (uint32_t y = 0; y < 8u; ++y) {
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)extra, (int)y);
+        if (y < lane) base += e;
+    }
+    if (lane == 0) bc[8u * n_blk] = m;
+    if (lane < 8u) bc[8u * n_blk + 1u + lane] = base;
+}
+
+__global__ __launch_bounds__(kXgBlock) void xg_place_kernel(const uint32_t *in, uint32_t *out, uint32_t n,
+                                                            const unsigned long long *live_tiles, const uint32_t *bc,
+                                                            uint32_t n_blk) {
+    __shared__ uint32_t wc[kXgWaves][8];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, i = blockIdx.x * kXgBlock + threadIdx.x;
+    const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
+    const uint32_t x = xg_group(in, i, L);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t rank = 0;
+    for (uint32_t v = 0; v < 8u; ++v) {
+        const uint64_t m = __ballot(x == v);
+        if (x == v) rank = (uint32_t)__popcll(m & lt);
+        if (lane == v) wc[wave][v] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (i >= n) return;
+    if (x >= 8u) {  // a dead tile's unit (or past the live prefix): unchanged
+        out[i] = in[i];
+        return;
+    }
+    for (uint32_t w = 0; w < wave; ++w) rank += wc[w][x];
+    const uint32_t r = bc[8u * blockIdx.x + x] + rank;
+    const uint32_t m = bc[8u * n_blk];
+    const uint32_t pos = r < m ? 8u * r + x : 8u * m + bc[8u * n_blk + 1u + x] + (r - m);
+    out[pos] = in[i];
+}
+
 #endif  // !RTK_P16_TU
 }  // namespace rtk
 
@@ -1973,6 +2060,18 @@ extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *s
     hipLaunchKernelGGL(rtk::tile_count_kernel, grid, block, 0, stream, (const uint32_t *)cost, n, scratch);
     hipLaunchKernelGGL(rtk::tile_scan_kernel, dim3(1), dim3(1024), 0, stream, scratch, n_blk);
     hipLaunchKernelGGL(rtk::tile_rank_kernel, grid, block, 0, stream, cost, n, (const uint32_t *)scratch, order);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int rtk_launch_xcd_group(const uint32_t *order_in, uint32_t *order_out, uint32_t n_units,
+                                    const unsigned long long *live_tiles, uint32_t *scratch, hipStream_t stream) {
+    const uint32_t n_blk = (n_units + rtk::kXgBlock - 1u) / rtk::kXgBlock;
+    if (n_blk == 0) return 0;
+    hipLaunchKernelGGL(rtk::xg_count_kernel, dim3(n_blk), dim3(rtk::kXgBlock), 0, stream, order_in, n_units, live_tiles,
+                       scratch);
+    hipLaunchKernelGGL(rtk::xg_scan_kernel, dim3(1), dim3(64), 0, stream, scratch, n_blk);
+    hipLaunchKernelGGL(rtk::xg_place_kernel, dim3(n_blk), dim3(rtk::kXgBlock), 0, stream, order_in, order_out, n_units,
+                       live_tiles, (const uint32_t *)scratch, n_blk);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
