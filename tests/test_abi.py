@@ -157,3 +157,40 @@ def test_scene_size_limits(rt):
         rt.scene_prefilter(rt.scene_from_spheres(sp[:]), True)
     r2, _, _ = rt.scene_prefilter(rt.scene_from_spheres(sp[:4 * 265 + 1]), True)  # one past the LDS image
     assert len(r2) == 4 * 266
+
+
+def test_frame_hash_is_the_fixtures_fnv1a(rt, orc):
+    """rt_frame_hash (the bench's frame check) is the FNV-1a 64 the committed
+    fixtures hold (the oracle's or_fnv1a64), on empty, odd-sized and random
+    buffers."""
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 7, 4096, 100003):
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        assert rt.frame_hash(a) == orc.fnv1a64(a), n
+    assert rt.frame_hash(np.zeros(0, np.uint8)) == 0xcbf29ce484222325
+
+
+def test_bench_finds_the_fixture_of_each_preset():
+    """bench.py checks its last timed frame against the committed fixture of
+    the workload (golden_for): C2, C3, RTWeekend and C2-inside each have one,
+    a custom workload has none."""
+    import sys
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    class A:
+        pass
+    for cfg, name in (("c2", "c2_full_1920x1080x256"), ("c3", "c3_full_3840x2160x1024"),
+                      ("rtw", "rtw_full_1920x1080x64"), ("c2in", "c2in_full_1920x1080x256")):
+        a = A()
+        for k, v in bench.CONFIGS[cfg].items():
+            setattr(a, k, v)
+        a.scalar = False
+        n = 482 if cfg == "rtw" else a.spheres
+        got, g = bench.golden_for(a, a.width, a.height, a.spp, n, a.bounces)
+        assert got == name, (cfg, got)
+        assert g["seed_mode"] == "pixel"
+    a.spp = 3
+    assert bench.golden_for(a, a.width, a.height, a.spp, 64, a.bounces) == (None, None)
+    assert bench.combine_verified(None, True) is True and bench.combine_verified(True, False) is False
+    assert bench.combine_verified(None, None) is None
