@@ -131,11 +131,12 @@ def test_one_frame_launches_take_four_pixels_per_lane(rt, orc, torch_cuda, gdev,
             assert np.array_equal(g[1].cpu().numpy().view(np.uint32), oc), (r, k)
 
 
-@pytest.mark.parametrize("order", ["1", "0"])
+@pytest.mark.parametrize("order,xcd,seg", [("1", "1", "1"), ("1", "0", "1"), ("0", "1", "1"), ("1", "1", "2"),
+                                            ("1", "1", "4")])
 @pytest.mark.parametrize("scene_idx,n,W,H,spp,B,lpp", [(1, 64, 96, 80, 8, 8, "4"), (2, None, 72, 56, 8, 5, "4"),
                                                        (0, None, 64, 48, 16, 5, "8"), (1, 200, 40, 32, 16, 8, "16")])
 def test_pixels_dealt_by_cost_keep_every_bit(rt, orc, torch_cuda, monkeypatch, scene_idx, n, W, H, spp, B, lpp,
-                                             order):
+                                             order, xcd, seg):
     """RT_PIXEL_SORT=1: after a launch measures each pixel's traced segments,
     every block tile's pixels are dealt to its four waves cheapest first (and
     a permuted wave tests the union of the block's quadrant masks).  Repeated
@@ -143,6 +144,8 @@ def test_pixels_dealt_by_cost_keep_every_bit(rt, orc, torch_cuda, monkeypatch, s
     monkeypatch.setenv("RT_PIXEL_SORT", "1")
     monkeypatch.setenv("RT_LANES_PER_PIXEL", lpp)
     monkeypatch.setenv("RT_WAVE_ORDER", order)  # waves ordered by cost, or block tiles
+    monkeypatch.setenv("RT_XCD_GROUP", xcd)  # a block tile's waves grouped onto one XCD (wave order only)
+    monkeypatch.setenv("RT_PIXEL_SEG", seg)  # pixels dealt singly, in pairs or in 4-pixel row segments
     dev = rt.Device(0)
     try:
         s, o = _scenes(rt, orc, scene_idx, n)
@@ -389,7 +392,10 @@ VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0
                 # merged primary/secondary rounds forced on (every per-group-walk kernel) and off
                 {"RT_MERGE_ROUNDS": "1", "RT_CLUSTERS": "0"}, {"RT_MERGE_ROUNDS": "0"}, {"RT_PIXEL_SORT": "0"},
                 # block tiles ordered by cost instead of waves
-                {"RT_WAVE_ORDER": "0"}]
+                {"RT_WAVE_ORDER": "0"},
+                # round 5: RGBA8 stored by the trace kernel (no encode pass); pixel pairs / 4-pixel
+                # row segments dealt by cost; waves not grouped by XCD
+                {"RT_CUR_PASS": "0"}, {"RT_PIXEL_SEG": "2"}, {"RT_PIXEL_SEG": "4"}, {"RT_XCD_GROUP": "0"}]
 
 
 @pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
