@@ -520,8 +520,9 @@ int rt_on_render_get_profile(rt_on_render_profile *out, int reset);
  * resize within that size frees and allocates nothing: it re-uses them, as
  * the reference re-Pushes its images into the arena OnInit sized (main.cpp:
  * 658, 798-804).  rt_on_init reserves its 1280x720 window (main.cpp:649-650).
- * Keeps the current frames; on several devices a reservation that grows their
- * resident means restarts the running mean at the next call.  New. */
+ * Keeps the current frames on one device; on several devices (rt_on_init_devices)
+ * the call restarts the running mean at the next rt_on_render, as a resize does,
+ * since growing the devices' resident means drops them.  New. */
 int rt_on_render_reserve(uint32_t width, uint32_t height);
 
 /* ----------------------------------------------------------- output path */

@@ -85,7 +85,6 @@ struct App {
     // reference re-Pushes its images into the arena OnInit sized (main.cpp:
     // 658, 798-804): no call of the frame loop frees or allocates.
     size_t cap_px = 0;
-    uint32_t reserve_w = 0, reserve_h = 0;  // launch buffers reserved for this geometry (0: none)
     bool restart_pending = false;  // a reservation dropped the resident mean: the next call restarts it
     uint32_t slot = 0;             // d_cur slot of the last launched frame
     uint64_t *d_rays = nullptr;
@@ -145,8 +144,12 @@ int ensure_frames(size_t px) {
     if (live && g_app.d_prev &&
         (hipMemcpy(prev, g_app.d_prev, live * 16u, hipMemcpyDeviceToDevice) != hipSuccess ||
          hipMemcpy(cur[0], g_app.d_cur[0], live * 4u, hipMemcpyDeviceToDevice) != hipSuccess ||
-         hipMemcpy(cur[1], g_app.d_cur[1], live * 4u, hipMemcpyDeviceToDevice) != hipSuccess))
+         hipMemcpy(cur[1], g_app.d_cur[1], live * 4u, hipMemcpyDeviceToDevice) != hipSuccess)) {
+        (void)hipFree(prev);  // the old frames stay in place
+        (void)hipFree(cur[0]);
+        (void)hipFree(cur[1]);
         return RT_EIO;
+    }
     (void)hipFree(g_app.d_prev);
     (void)hipFree(g_app.d_cur[0]);
     (void)hipFree(g_app.d_cur[1]);
@@ -159,22 +162,21 @@ int ensure_frames(size_t px) {
 }
 
 // The trace's launch buffers for a width x height frame (rt_device_reserve, or
-// rt_multi_reserve over the devices' 8-row bands), once per geometry.
+// rt_multi_reserve over the devices' 8-row bands).  Called for every new
+// geometry: a reservation already covering it grows nothing (the libraries keep
+// the largest tile and pixel counts asked for), and only a new geometry gets here.
 int reserve_launch(uint32_t w, uint32_t h) {
-    if (w <= g_app.reserve_w && h <= g_app.reserve_h) return RT_OK;
     int rc;
     if (g_app.multi) {
         rc = rt_multi_reserve(g_app.multi, w, h, 8u, 0u);
-        // a grown device mean is gone (rt_multi_reserve): restart it next call
+        // a reservation that grows the devices' resident means drops them (rt_multi_reserve):
+        // restart the mean at the next call (a resize restarts it anyway)
         if (g_app.width && g_app.prev_count) g_app.restart_pending = true;
     } else {
         rc = rt_device_reserve(g_app.dev, w, h);
     }
-    if (rc) return rc;
-    g_app.reserve_w = std::max(g_app.reserve_w, w);
-    g_app.reserve_h = std::max(g_app.reserve_h, h);
     (void)hipSetDevice(g_app.ordinal);
-    return RT_OK;
+    return rc;
 }
 
 void unregister_image() {
@@ -264,7 +266,6 @@ extern "C" int rt_on_render_reserve(uint32_t width, uint32_t height) {
         return RT_EINVAL;
     if (hipSetDevice(g_app.ordinal) != hipSuccess) return RT_ENODEV;
     const size_t px = (size_t)width * height;
-    if (px <= g_app.cap_px && width <= g_app.reserve_w && height <= g_app.reserve_h) return RT_OK;
     if (wait_frame() != RT_OK) return RT_EIO;  // growing frees buffers the frame in flight uses
     if (const int rc = ensure_frames(px)) return rc;
     return reserve_launch(width, height);
