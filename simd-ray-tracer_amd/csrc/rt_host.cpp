@@ -85,6 +85,7 @@ struct rt_device {
     uint32_t order_launches = 6;      // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept
     uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
     uint32_t *d_tile_order_sorted = nullptr;  // the sort's output before XCD grouping (rtk_launch_xcd_group)
+    uint32_t *d_tile_aux = nullptr;           // XCD grouping: per block tile, first sorted position and group
     uint32_t *d_tile_live = nullptr;
     unsigned long long *d_cull_counters = nullptr;  // kCullCounterWords: striped counters + device totals of the cull pass
     uint64_t *d_masks = nullptr;  // cull pass output: per wave tile primary group masks
@@ -254,6 +255,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipFree(d->d_tile_cost);
     (void)hipFree(d->d_tile_order);
     (void)hipFree(d->d_tile_order_sorted);
+    (void)hipFree(d->d_tile_aux);
     (void)hipFree(d->d_tile_scratch);
     (void)hipFree(d->d_tile_live);
     (void)hipFree(d->d_cull_counters);
@@ -967,7 +969,7 @@ static int ensure_tile_buffers(rt_device *d, uint32_t n_tiles, hipStream_t sync,
     else HIP_OK(hipStreamSynchronize(sync));
     if (n_tiles > d->tile_cap) {
         for (uint32_t **b : {&d->d_tile_cost, &d->d_tile_order, &d->d_tile_scratch, &d->d_tile_live,
-                             &d->d_tile_order_sorted}) {
+                             &d->d_tile_order_sorted, &d->d_tile_aux}) {
             (void)hipFree(*b);
             *b = nullptr;
         }
@@ -976,6 +978,7 @@ static int ensure_tile_buffers(rt_device *d, uint32_t n_tiles, hipStream_t sync,
         if (hipMalloc(&d->d_tile_cost, 4u * n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_order, 4u * n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_order_sorted, 4u * n_tiles * 4u) != hipSuccess ||
+            hipMalloc(&d->d_tile_aux, 2u * n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_live, n_tiles * 4u) != hipSuccess ||
             hipMalloc(&d->d_tile_scratch, rtk_tile_sort_scratch(4u * n_tiles)) != hipSuccess)
             return fail(RT_ENOMEM, "rt_trace: tile order buffers");
@@ -1347,7 +1350,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             if (rtk_launch_tile_sort(d->d_tile_cost, group ? d->d_tile_order_sorted : d->d_tile_order,
                                      d->d_tile_scratch, n_units, s) != 0 ||
                 (group && rtk_launch_xcd_group(d->d_tile_order_sorted, d->d_tile_order, n_units,
-                                               d->d_cull_counters + kCullTotals, d->d_tile_scratch, s) != 0))
+                                               d->d_cull_counters + kCullTotals, d->d_tile_scratch, d->d_tile_aux,
+                                               s) != 0))
                 return fail(RT_EIO, "rt_trace: tile sort launch failed: %s", hipGetErrorString(hipGetLastError()));
             if (pixel_sort && rtk_launch_pixel_sort(&a, lpp, d->d_pix_perm, s) != 0)
                 return fail(RT_EIO, "rt_trace: pixel sort launch failed: %s", hipGetErrorString(hipGetLastError()));

@@ -152,11 +152,13 @@ extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull,
 extern "C" size_t rtk_tile_sort_scratch(uint32_t n);
 extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *scratch, uint32_t n, hipStream_t stream);
 // One-wave kernels' wave order: the live prefix (4 x live_tiles[0] units) of a sorted
-// order_in partitioned stably by XCD group (block tile & 7) and interleaved so that
-// every wave of a block tile runs on one XCD (rt_kernel.hip, "XCD grouping"); the
-// rest copied.  scratch: rtk_tile_sort_scratch(n_units) bytes (8 n_blk + 9 words used).
+// order_in partitioned stably by XCD group (every eighth live tile by its heaviest
+// wave's rank) and interleaved so that every wave of a block tile runs on one XCD
+// (rt_kernel.hip, "XCD grouping"); the rest copied.  scratch: rtk_tile_sort_scratch(
+// n_units) bytes (8 n_blk + 9 words used); aux: 2 x n_units / 4 words.
 extern "C" int rtk_launch_xcd_group(const uint32_t *order_in, uint32_t *order_out, uint32_t n_units,
-                                    const unsigned long long *live_tiles, uint32_t *scratch, hipStream_t stream);
+                                    const unsigned long long *live_tiles, uint32_t *scratch, uint32_t *aux,
+                                    hipStream_t stream);
 extern "C" uint32_t rtk_tile_count(uint32_t width, uint32_t local_rows, int lanes_per_pixel);
 extern "C" uint32_t rtk_tiles_x(uint32_t width, int lanes_per_pixel);
 // grid: blocks of the trace launch (tile_order[0..grid) when tile_order is set)

@@ -1964,7 +1964,7 @@ __global__ __launch_bounds__(kSortBlock) void tile_rank_kernel(uint32_t *cost, u
 // neighbouring pixels of the same 128-B lines, land on up to four XCDs whose
 // L2s each write their part of every line back (the excess HBM writes of §4).
 // Grouping keeps the per-wave heaviest-first order but moves every unit of block
-// tile t into XCD group x = t & 7: the live prefix [0, L) of the sorted order is
+// tile t into one XCD group x = grp[t] (below): the live prefix [0, L) of the sorted order is
 // partitioned stably by x (each group stays heaviest first), and group x's r-th
 // unit goes to position 8r + x while r < m (the smallest group's size), so block
 // 8r + x runs on the group's XCD; the r >= m leftovers (the lightest units of the
@@ -1972,16 +1972,78 @@ __global__ __launch_bounds__(kSortBlock) void tile_rank_kernel(uint32_t *cost, u
 // no unit is lost or repeated; [L, n) (dead tiles' units) is copied as is.
 constexpr uint32_t kXgBlock = 1024, kXgWaves = kXgBlock / 64;
 
-__device__ __forceinline__ uint32_t xg_group(const uint32_t *in, uint32_t i, uint32_t live_units) {
-    return i < live_units ? (in[i] >> 2) & 7u : 8u;
+// The group of a block tile is its rank, among the live tiles, in the order of
+// their heaviest wave (the tile's first unit in the sorted order), modulo 8: the
+// groups then take every eighth tile of a cost-sorted list, so the eight XCDs get
+// equal work (a group by tile & 7 measured C2 -1.2 %: its columns' costs differ).
+// xg_first_kernel: first[t] = the smallest sorted position of tile t's units;
+// xg_flag_count / xg_scan / xg_tile_rank: grp[t] = (rank of tile t among the live
+// tiles, by first[t]) & 7 (first and grp: two n_tiles-word arrays in aux).
+__device__ __forceinline__ uint32_t xg_group(const uint32_t *in, uint32_t i, uint32_t live_units,
+                                             const uint32_t *grp) {
+    return i < live_units ? grp[in[i] >> 2] : 8u;
+}
+
+__global__ __launch_bounds__(kXgBlock) void xg_first_kernel(const uint32_t *in, uint32_t n,
+                                                            const unsigned long long *live_tiles, uint32_t *first) {
+    const uint32_t i = blockIdx.x * kXgBlock + threadIdx.x;
+    const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
+    if (i < L) atomicMin(first + (in[i] >> 2), i);
+}
+
+// per block: the number of positions that are their tile's first (bc[blk])
+__global__ __launch_bounds__(kXgBlock) void xg_flag_count_kernel(const uint32_t *in, uint32_t n,
+                                                                 const unsigned long long *live_tiles,
+                                                                 const uint32_t *first, uint32_t *bc) {
+    __shared__ uint32_t wc[kXgWaves];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, i = blockIdx.x * kXgBlock + threadIdx.x;
+    const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
+    const bool f = i < L && first[in[i] >> 2] == i;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kXgWaves; ++w) t += wc[w];
+        bc[blockIdx.x] = t;
+    }
+}
+
+// one wave: exclusive scan of bc[0, n_blk) in place
+__global__ __launch_bounds__(64) void xg_scan1_kernel(uint32_t *bc, uint32_t n_blk) {
+    if (threadIdx.x != 0) return;
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < n_blk; ++b) {
+        const uint32_t c = bc[b];
+        bc[b] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(kXgBlock) void xg_tile_rank_kernel(const uint32_t *in, uint32_t n,
+                                                                const unsigned long long *live_tiles,
+                                                                const uint32_t *first, const uint32_t *bc,
+                                                                uint32_t *grp) {
+    __shared__ uint32_t wc[kXgWaves];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, i = blockIdx.x * kXgBlock + threadIdx.x;
+    const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
+    const bool f = i < L && first[in[i] >> 2] == i;
+    const uint64_t m = __ballot(f);
+    if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (!f) return;
+    uint32_t rank = bc[blockIdx.x] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    for (uint32_t w = 0; w < wave; ++w) rank += wc[w];
+    grp[in[i] >> 2] = rank & 7u;
 }
 
 __global__ __launch_bounds__(kXgBlock) void xg_count_kernel(const uint32_t *in, uint32_t n,
-                                                            const unsigned long long *live_tiles, uint32_t *bc) {
+                                                            const unsigned long long *live_tiles, const uint32_t *grp,
+                                                            uint32_t *bc) {
     __shared__ uint32_t wc[kXgWaves][8];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, i = blockIdx.x * kXgBlock + threadIdx.x;
     const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
-    const uint32_t x = xg_group(in, i, L);
+    const uint32_t x = xg_group(in, i, L, grp);
     for (uint32_t v = 0; v < 8u; ++v) {
         const uint64_t m = __ballot(x == v);
         if (lane == v) wc[wave][v] = (uint32_t)__popcll(m);
@@ -2019,12 +2081,12 @@ __global__ __launch_bounds__(64) void xg_scan_kernel(uint32_t *bc, uint32_t n_bl
 }
 
 __global__ __launch_bounds__(kXgBlock) void xg_place_kernel(const uint32_t *in, uint32_t *out, uint32_t n,
-                                                            const unsigned long long *live_tiles, const uint32_t *bc,
-                                                            uint32_t n_blk) {
+                                                            const unsigned long long *live_tiles, const uint32_t *grp,
+                                                            const uint32_t *bc, uint32_t n_blk) {
     __shared__ uint32_t wc[kXgWaves][8];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, i = blockIdx.x * kXgBlock + threadIdx.x;
     const uint32_t L = (uint32_t)min((unsigned long long)n, 4ull * *live_tiles);
-    const uint32_t x = xg_group(in, i, L);
+    const uint32_t x = xg_group(in, i, L, grp);
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t rank = 0;
     for (uint32_t v = 0; v < 8u; ++v) {
@@ -2064,14 +2126,25 @@ extern "C" int rtk_launch_tile_sort(uint32_t *cost, uint32_t *order, uint32_t *s
 }
 
 extern "C" int rtk_launch_xcd_group(const uint32_t *order_in, uint32_t *order_out, uint32_t n_units,
-                                    const unsigned long long *live_tiles, uint32_t *scratch, hipStream_t stream) {
+                                    const unsigned long long *live_tiles, uint32_t *scratch, uint32_t *aux,
+                                    hipStream_t stream) {
     const uint32_t n_blk = (n_units + rtk::kXgBlock - 1u) / rtk::kXgBlock;
     if (n_blk == 0) return 0;
-    hipLaunchKernelGGL(rtk::xg_count_kernel, dim3(n_blk), dim3(rtk::kXgBlock), 0, stream, order_in, n_units, live_tiles,
-                       scratch);
+    const uint32_t n_tiles = (n_units + 3u) / 4u;
+    uint32_t *first = aux, *grp = aux + n_tiles;
+    const dim3 grid(n_blk), block(rtk::kXgBlock);
+    if (hipMemsetAsync(first, 0xFF, (size_t)n_tiles * 4u, stream) != hipSuccess) return -5;
+    hipLaunchKernelGGL(rtk::xg_first_kernel, grid, block, 0, stream, order_in, n_units, live_tiles, first);
+    hipLaunchKernelGGL(rtk::xg_flag_count_kernel, grid, block, 0, stream, order_in, n_units, live_tiles,
+                       (const uint32_t *)first, scratch);
+    hipLaunchKernelGGL(rtk::xg_scan1_kernel, dim3(1), dim3(64), 0, stream, scratch, n_blk);
+    hipLaunchKernelGGL(rtk::xg_tile_rank_kernel, grid, block, 0, stream, order_in, n_units, live_tiles,
+                       (const uint32_t *)first, (const uint32_t *)scratch, grp);
+    hipLaunchKernelGGL(rtk::xg_count_kernel, grid, block, 0, stream, order_in, n_units, live_tiles,
+                       (const uint32_t *)grp, scratch);
     hipLaunchKernelGGL(rtk::xg_scan_kernel, dim3(1), dim3(64), 0, stream, scratch, n_blk);
-    hipLaunchKernelGGL(rtk::xg_place_kernel, dim3(n_blk), dim3(rtk::kXgBlock), 0, stream, order_in, order_out, n_units,
-                       live_tiles, (const uint32_t *)scratch, n_blk);
+    hipLaunchKernelGGL(rtk::xg_place_kernel, grid, block, 0, stream, order_in, order_out, n_units, live_tiles,
+                       (const uint32_t *)grp, (const uint32_t *)scratch, n_blk);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
