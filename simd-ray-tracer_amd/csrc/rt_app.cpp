@@ -13,8 +13,6 @@
 // RT_KEY_* bits the caller passes instead of the platform's IsDown().
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
-
-#include <algorithm>
 #include <string.h>
 #include <time.h>
 
