@@ -66,7 +66,6 @@ struct rt_device {
     // RT_XCD_GROUP: every wave of a block tile on one XCD (rtk_launch_xcd_group), so its lines'
     // partial stores merge in one L2 before they are written back
     int xcd_group_env = 1;
-    uint32_t spread_s = 0, spread_h = 0;  // RT_HEAVY_SPREAD / RT_HEAVY_COUNT (experiment, TraceArgs.spread_*)
     // RGBA8 encoded from the running mean by a coalesced pass after the launch (TraceArgs.skip_cur),
     // at P >= 2: trace-kernel HBM writes C2 21.0 -> 15.7 MB, RTWeekend 80.6 -> 54.1 MB, C2 +0.7 %
     // (profiles/r05e_cur_pass_ab.txt); RT_CUR_PASS=0 stores RGBA8 in the trace kernel
@@ -226,8 +225,6 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     if (psort && (psort[0] == '0' || psort[0] == '1')) d->pixel_sort_env = psort[0] - '0';
     const char *cps = getenv("RT_CUR_PASS");
     if (cps && (cps[0] == '0' || cps[0] == '1')) d->cur_pass = (uint32_t)(cps[0] - '0');
-    if (const char *hs = getenv("RT_HEAVY_SPREAD")) d->spread_s = (uint32_t)std::max(0, atoi(hs));
-    if (const char *hc = getenv("RT_HEAVY_COUNT")) d->spread_h = (uint32_t)std::max(0, atoi(hc));
     const char *xg = getenv("RT_XCD_GROUP");
     if (xg && (xg[0] == '0' || xg[0] == '1')) d->xcd_group_env = xg[0] - '0';
     const char *pseg = getenv("RT_PIXEL_SEG");
@@ -1338,14 +1335,6 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         // per-wave 4-B cost stores (scattered partial lines, ~8 MB of HBM writes per 1080p
         // launch at P = 4) would feed nothing
         a.tile_cost = resort ? d->d_tile_cost : nullptr;
-        // heavy spread only over a known grid (no early-exit blocks): H per XCD queue, capped so
-        // that S x H slots fit the shortest queue
-        {
-            const uint32_t grid_units = grid_tiles * (a.solo ? 4u : 1u);
-            const uint32_t S = d->spread_s, qmin = grid_units / 8u;
-            a.spread_s = known && a.tile_order && S > 1u ? S : 0u;
-            a.spread_h = a.spread_s ? std::min(d->spread_h, qmin / S) : 0u;
-        }
         if (rtk_launch_trace_grid(&a, desc->EnableSIMD ? 1 : 0, src, cull ? 1 : 0, lpp, grid_tiles, s) != 0)
             return fail(RT_EIO, "rt_trace: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
         if (any_dead && rtk_launch_empty(&a, lpp, d->d_tile_live, d->d_cull_counters + kCullTotals + 1, s) != 0)

@@ -104,8 +104,6 @@ struct TraceArgs {
     // encoded from it by one coalesced pass after the launch (rtk_launch_encode), so its 4-B
     // pixels are not written as scattered partial lines from several XCDs (RT_CUR_PASS)
     uint32_t skip_cur;
-    // experiment (RT_HEAVY_SPREAD=S, RT_HEAVY_COUNT=H): see trace_kernel; 0 = off
-    uint32_t spread_s, spread_h;
 };
 constexpr uint32_t kMergeGroups = 2;
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)

@@ -1055,20 +1055,7 @@ void trace_kernel(TraceArgs a) {
     uint32_t tile, wave;
     const bool unit_waves = SOLO && a.unit_waves != 0u;
     if (unit_waves) {
-        // heavy spread (experiment, TraceArgs.spread_s): within each XCD's queue (blocks
-        // b = 8q + x), the heaviest spread_h units take every spread_s-th slot at issue
-        // priority 3 and lighter units fill the slots between, so a SIMD holds about one
-        // heavy wave beside light ones instead of several heavy ones sharing its issue
-        uint32_t b = blockIdx.x;
-        if (a.spread_s > 1u && a.tile_order) {
-            const uint32_t x = b & 7u, q = b >> 3, S = a.spread_s, H = a.spread_h;
-            if (q < S * H) {
-                const bool heavy = q % S == 0u;
-                b = 8u * (heavy ? q / S : H + q - q / S - 1u) + x;
-                if (heavy) __builtin_amdgcn_s_setprio(3);
-            }
-        }
-        const uint32_t u = a.tile_order ? a.tile_order[b] : b;
+        const uint32_t u = a.tile_order ? a.tile_order[blockIdx.x] : blockIdx.x;
         tile = u >> 2;
         wave = u & 3u;
     } else {
