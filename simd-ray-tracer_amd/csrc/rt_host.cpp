@@ -20,6 +20,8 @@ struct rt_device {
     bool lut_set = false;
     // SIMD rule set (SIMDSpheres + Materials) and scalar rule set (ScalarSpheres)
     float4 *d_groups[2] = {nullptr, nullptr};
+    // the primary rounds' camera-relative group rows (TraceArgs.prim), written by the cull pass
+    float4 *d_prim[2] = {nullptr, nullptr};
     float4 *d_mats[2] = {nullptr, nullptr};
     uint32_t n_groups[2] = {0, 0};
     uint32_t n_spheres = 0;
@@ -246,6 +248,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
     (void)hipDeviceSynchronize();
     for (int r = 0; r < 2; ++r) {
         (void)hipFree(d->d_groups[r]);
+        (void)hipFree(d->d_prim[r]);
         (void)hipFree(d->d_mats[r]);
         (void)hipFree(d->d_clusters[r]);
     }
@@ -322,11 +325,14 @@ static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, co
     if (n_groups > d->cap_groups[rs]) {
         (void)hipFree(d->d_groups[rs]);
         (void)hipFree(d->d_mats[rs]);
+        (void)hipFree(d->d_prim[rs]);
         d->d_groups[rs] = nullptr;
         d->d_mats[rs] = nullptr;
+        d->d_prim[rs] = nullptr;
         // +2 padding groups: the kernel's loops prefetch up to group g+2 while testing g
         if (hipMalloc(&d->d_groups[rs], (size_t)(n_groups + 2) * kGroupF4 * 16) != hipSuccess ||
-            hipMalloc(&d->d_mats[rs], (size_t)n_groups * 128) != hipSuccess)
+            hipMalloc(&d->d_mats[rs], (size_t)n_groups * 128) != hipSuccess ||
+            hipMalloc(&d->d_prim[rs], (size_t)n_groups * kPrimF4 * 16) != hipSuccess)
             return fail(RT_ENOMEM, "rt_scene_upload: device allocation failed");
         d->cap_groups[rs] = n_groups;
     }
@@ -1243,6 +1249,8 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     if (pixel_sort)
         if (const int rc = ensure_pixel_sort(d, n_tiles, (size_t)desc->Width * local_rows, s, false)) return rc;
     const bool new_key = key != d->tile_key;
+    // (the table is written by the key's cull pass: the key holds the camera and the scene)
+    a.prim = cull ? d->d_prim[rs] : nullptr;
     uint32_t head_frames = 0;  // > 0: split this launch (first launch of a key, below): frames of the leading parts
     uint32_t split[8], n_split = 0;
     if (new_key) {

@@ -104,7 +104,13 @@ struct TraceArgs {
     // encoded from it by one coalesced pass after the launch (rtk_launch_encode), so its 4-B
     // pixels are not written as scattered partial lines from several XCDs (RT_CUR_PASS)
     uint32_t skip_cur;
+    // CULL (required): the primary rounds' group rows, written by the cull pass for its camera
+    // (rtk_launch_cull): per group kPrimF4 float4 = {cx[4]}, {cy[4]}, {cz[4]}, {r*r[4]} with
+    // c = RN(centre - CameraPosition), the first three f32 ops of every primary sphere test
+    // (main.cpp:401), identical on every lane of a primary round (one s_load_dwordx16)
+    float4 *prim;
 };
+constexpr uint32_t kPrimF4 = 4;
 constexpr uint32_t kMergeGroups = 2;
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)
 // striped image pixels of dead block tiles, then the two totals at kCullTotals
@@ -164,7 +170,8 @@ extern "C" uint32_t rtk_tiles_x(uint32_t width, int lanes_per_pixel);
 // grid: blocks of the trace launch (tile_order[0..grid) when tile_order is set)
 extern "C" int rtk_launch_trace_grid(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,
                                      uint32_t grid, hipStream_t stream);
-// Primary-ray cone culling of every wave tile -> a->masks (must be set);
+// Primary-ray cone culling of every wave tile -> a->masks, and the camera-relative
+// group rows of the primary rounds -> a->prim (both must be set);
 // per block tile live[t] (some wave tile has a candidate group, or
 // !empty_capable) and cost[t] = live ? 2 : 0 (so a tile sort puts live tiles
 // first); counters[0, 64) sum to the live tiles, counters[64, 128) to the

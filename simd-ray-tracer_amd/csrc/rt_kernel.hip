@@ -834,6 +834,62 @@ __device__ __forceinline__ void test_group(const TraceArgs &a, const Group &G, u
     }
 }
 
+// pair_dist for rays that all start at the camera (primary rounds): C = S - O
+// is the same on every lane, so its three packed subtractions come from the
+// cull pass's table (TraceArgs.prim, computed with the same single f32
+// rounding) and the C operands stay in SGPRs -- 16 packed ops instead of 19.
+__device__ __forceinline__ f2 pair_dist_c(const RayPk &r, f2 cx, f2 cy, f2 cz, f2 &T) {
+    f2 qx, qy, qz, t, d;
+    asm("v_pk_mul_f32 %[t], %[cx], %[rx] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_mul_f32 %[d], %[cy], %[ry] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[T], %[t], %[d]\n\t"
+        "v_pk_mul_f32 %[t], %[cz], %[rz] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[T], %[T], %[t]\n\t"
+        "v_pk_mul_f32 %[t], %[rx], %[T] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[qx], %[cx], %[t] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[t], %[ry], %[T] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[qy], %[cy], %[t] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[t], %[rz], %[T] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f32 %[qz], %[cz], %[t] neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %[d], %[qx], %[qx]\n\t"
+        "v_pk_mul_f32 %[t], %[qy], %[qy]\n\t"
+        "v_pk_add_f32 %[d], %[d], %[t]\n\t"
+        "v_pk_mul_f32 %[t], %[qz], %[qz]\n\t"
+        "v_pk_add_f32 %[d], %[d], %[t]"
+        : [qx] "=&v"(qx), [qy] "=&v"(qy), [qz] "=&v"(qz), [t] "=&v"(t), [T] "=&v"(T), [d] "=&v"(d)
+        : [cx] "s"(cx), [cy] "s"(cy), [cz] "s"(cz), [rx] "v"(r.x), [ry] "v"(r.y), [rz] "v"(r.z));
+    return d;
+}
+
+// test_group for a primary round: group g's camera-relative rows (TraceArgs.prim).
+template <bool SIMD>
+__device__ __forceinline__ void test_group_prim(const TraceArgs &a, cv4f_t *prim, uint32_t g, const RayPk &p, Hit &h) {
+    cv4f_t *pg = prim + kPrimF4 * g;
+    const v4f_t cx = pg[0], cy = pg[1], cz = pg[2], r2 = pg[3];
+    f2 T01, T23;
+    const f2 d01 = pair_dist_c(p, f2{cx.x, cx.y}, f2{cy.x, cy.y}, f2{cz.x, cz.y}, T01);
+    const f2 d23 = pair_dist_c(p, f2{cx.z, cx.w}, f2{cy.z, cy.w}, f2{cz.z, cz.w}, T23);
+    bool h0, h1, h2, h3;
+    if (SIMD) {  // HitMask = d < r^2 (main.cpp:409)
+        h0 = d01.x < r2.x;
+        h1 = d01.y < r2.y;
+        h2 = d23.x < r2.z;
+        h3 = d23.y < r2.w;
+    } else {  // !(d > r^2) over the Count real spheres only (main.cpp:547,557)
+        const uint32_t s0 = 4u * g;
+        h0 = s0 + 0u < a.n_spheres && !(d01.x > r2.x);
+        h1 = s0 + 1u < a.n_spheres && !(d01.y > r2.y);
+        h2 = s0 + 2u < a.n_spheres && !(d23.x > r2.z);
+        h3 = s0 + 3u < a.n_spheres && !(d23.y > r2.w);
+    }
+    if (h0 | h1 | h2 | h3) {
+        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x, a.fast_sqrt != 0u);
+        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y, a.fast_sqrt != 0u);
+        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z, a.fast_sqrt != 0u);
+        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w, a.fast_sqrt != 0u);
+    }
+}
+
 // Conservative per-wave culling for primary rays.  All primary rays of a
 // tile start at CameraPosition and point into the tile's film rectangle
 // (+-0.5 px jitter), i.e. inside a cone (axis A, half-angle theta).  A sphere
@@ -1415,6 +1471,10 @@ void trace_kernel(TraceArgs a) {
                     hit_reset(h);
                     const RayPk ray = {p.rx, p.ry, p.rz};
                     if (CULL && !do_sec && !merged) {
+                        // (the table's address is loaded here from the kernarg segment, as
+                        // the camera fields are: held in an SGPR pair across the trip loop it
+                        // cost the RTWeekend kernel SGPR spills, v_readlane in the loop)
+                        cv4f_t *prim = (cv4f_t *)kernel_args().prim;
                         for (uint32_t w = 0; w < n_words; ++w) {
                             // (readfirstlane returns int: widen each half as u32, or
                             // bit 31 would sign-extend into groups 32..63)
@@ -1426,7 +1486,7 @@ void trace_kernel(TraceArgs a) {
                             while (m) {
                                 const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
                                 m &= m - 1;
-                                test_group<SIMD>(a, load_group<SRC>(a, lds_groups, g), g, ray, h, nullptr);
+                                test_group_prim<SIMD>(a, prim, g, ray, h);
                             }
                         }
                     } else {
@@ -2276,10 +2336,29 @@ extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull,
         default: F<1>(__VA_ARGS__); break;                   \
     }
 
+namespace rtk {
+// The primary rounds' group rows for this camera (TraceArgs.prim): one sphere
+// slot per thread, c = RN(centre - CameraPosition) as main.cpp:401 rounds it
+// (one f32 subtraction: no contraction, IEEE denormals), and r*r copied.
+__global__ __launch_bounds__(256) void prim_kernel(TraceArgs a) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;  // sphere slot 4 g + l
+    if (i >= 4u * a.n_groups) return;
+    const uint32_t g = i >> 2, l = i & 3u;
+    const float *src = reinterpret_cast<const float *>(a.groups + (size_t)kGroupF4 * g);
+    float *dst = reinterpret_cast<float *>(a.prim + (size_t)kPrimF4 * g);
+    dst[0u + l] = src[4u * kRowX + l] - a.cam_pos[0];
+    dst[4u + l] = src[4u * kRowY + l] - a.cam_pos[1];
+    dst[8u + l] = src[4u * kRowZ + l] - a.cam_pos[2];
+    dst[12u + l] = src[4u * kRowR2 + l];
+}
+}  // namespace rtk
+
 template <int P>
 static void launch_cull_p(const TraceArgs *a, uint32_t *live, uint32_t *cost, unsigned long long *counters,
                           int empty_capable, hipStream_t stream) {
     const uint32_t n = rtk_tile_count(a->width, a->local_rows, P);
+    if (a->n_groups)
+        hipLaunchKernelGGL(rtk::prim_kernel, dim3((4u * a->n_groups + 255u) / 256u), dim3(256), 0, stream, *a);
     (void)hipMemsetAsync(counters, 0, 2u * rtk::kCullStripes * sizeof(unsigned long long), stream);
     hipLaunchKernelGGL(rtk::cull_kernel<P>, dim3(n), dim3(256), 0, stream, *a, live, cost, counters,
                        (uint32_t)(empty_capable != 0));
@@ -2288,7 +2367,7 @@ static void launch_cull_p(const TraceArgs *a, uint32_t *live, uint32_t *cost, un
 
 extern "C" int rtk_launch_cull(const TraceArgs *a, int lanes_per_pixel, uint32_t *live, uint32_t *cost,
                                unsigned long long *counters, int empty_capable, hipStream_t stream) {
-    if (!a->masks) return -1;
+    if (!a->masks || !a->prim) return -1;
     RTK_BY_P(launch_cull_p, a, live, cost, counters, empty_capable, stream)
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
