@@ -1493,13 +1493,15 @@ void trace_kernel(TraceArgs a) {
                         // Secondary rays: the prefiltered loop, whose error bound
                         // needs |D|^2 within 2^-16 of 1 on every lane (else exact).
                         const float u2 = __builtin_fmaf(p.rx.y, p.rx.y, __builtin_fmaf(p.ry.y, p.ry.y, p.rz.y * p.rz.y));
-                        const bool pf = do_sec && a.prefilter && !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
+                        // (a cluster-walk kernel runs only with the prefilter and a cluster table: rt_host.cpp)
+                        const bool pf = do_sec && (Walk<WALK>::CLUSTERS || a.prefilter) &&
+                                        !__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol));
                         if (kStats && a.stats && do_sec && !pf) {
                             st_sec_exact += 1;
                             st_sec_badlanes += __builtin_popcountll(__ballot(!(__builtin_fabsf(1.0f - u2) <= kPfDirTol)));
                             st_sec_zerodir += __builtin_popcountll(__ballot(u2 == 0.0f));
                         }
-                        if (SRC == kSrcSmem && pf && a.n_cpairs) {
+                        if (SRC == kSrcSmem && pf && (Walk<WALK>::CLUSTERS || a.n_cpairs)) {
                             if (kStats && a.stats) st_pf_rounds += 1;
                             PfStats *ps = kStats && a.stats ? &st_pf : nullptr;
                             if constexpr (Walk<WALK>::CLUSTERS) {
