@@ -84,7 +84,11 @@ struct rt_device {
     uint32_t head_samples = 8;        // samples per lane of the split's head (RT_HEAD_SAMPLES)
     uint32_t split_parts = 2;         // launches of a split first launch (RT_SPLIT_PARTS, <= 8)
     uint32_t split_growth = 3;        // each leading part this many times the previous (RT_SPLIT_GROWTH)
-    uint32_t order_launches = 6;      // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept
+    // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept.  4 (a key's split first launch
+    // sorts twice, then two more launches): as fast as 6 at steady state on C2 and the 8-rank share,
+    // 3 is slower (profiles/r05q_order_launches_ab.txt), and a bench's timed launches are past the
+    // sorting ones after two warm-ups
+    uint32_t order_launches = 4;
     uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
     uint32_t *d_tile_order_sorted = nullptr;  // the sort's output before XCD grouping (rtk_launch_xcd_group)
     uint32_t *d_tile_aux = nullptr;           // XCD grouping: per block tile, first sorted position and group
@@ -1348,7 +1352,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         if (any_dead && rtk_launch_empty(&a, lpp, d->d_tile_live, d->d_cull_counters + kCullTotals + 1, s) != 0)
             return fail(RT_EIO, "rt_trace: empty-tile launch failed: %s", hipGetErrorString(hipGetLastError()));
         // the learned order settles within a few launches (C2: 7.7, 6.3, 6.1, 5.9,
-        // 5.8 ms); after order_launches re-sorts (RT_ORDER_LAUNCHES, default 6)
+        // 5.8 ms); after order_launches re-sorts (RT_ORDER_LAUNCHES, default 4)
         // the order is kept and the three sort kernels (~14 us per launch, 1.5 %
         // of an 8-rank C2 share) are skipped
         if (resort) {
