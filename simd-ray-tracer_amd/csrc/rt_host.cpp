@@ -1140,9 +1140,11 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // sample hand-out, 40/44/48/52): RTWeekend (per-lane thresholds) 25.61k/25.73k/25.74k/
     // 25.71k, C5 (scene-wide) 52.74k/52.44k/52.58k/52.38k: 48 for per-lane walks.
     a.merge_rounds = d->merge_env == 1 || (d->merge_env == -1 && d->n_groups[rs] <= kMergeGroups) ? 1u : 0u;
+    // Round 5 (primary table, steady state): 24 for the small walks, against 16 / 32: C2 +1.2 %, C3 +1.0 %, the
+    // 4-rank share -2.7 %, the 8-rank share -0.8 % (profiles/r05r_sec_threshold_ab.txt).
     a.sec_threshold = d->sec_threshold;
     if (a.sec_threshold == 0)
-        a.sec_threshold = (a.clusters ? a.n_cpairs : a.n_groups) >= 12u ? (a.pf_relative ? 48u : 40u) : 16u;
+        a.sec_threshold = (a.clusters ? a.n_cpairs : a.n_groups) >= 12u ? (a.pf_relative ? 48u : 40u) : 24u;
     a.stats = d->d_stats;
     HIP_OK(hipSetDevice(d->ordinal));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
