@@ -670,6 +670,12 @@ __device__ __forceinline__ void merge_words(uint64_t (&wave)[kClWords], uint64_t
     }
 }
 
+// an SGPR pointer the compiler cannot see through: loads through it stay where they are written
+__device__ __forceinline__ cv4f_t *opaque(cv4f_t *p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
                                              uint64_t (&wave)[kClWords], PfStats *ps) {
@@ -679,7 +685,8 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
     for (uint32_t off = first * kEntryBytes; off != end; off += kEntryBytes) {
         cv4f_t *e = cl_entry(ct, off);
         const v4f_t r0 = e[0], r1 = e[1];
-        const v4f_t r2 = e[2], r3 = e[3];
+        const v4f_t r3 = e[3];
+        const v4f_t r2 = W <= 2 ? e[2] : v4f_t{0.0f, 0.0f, 0.0f, 0.0f};
         f2 T, cc;
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
         // a lane may hit the sphere: near the line, and not wholly behind the origin
@@ -695,18 +702,33 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         const uint64_t f0m = kBehind ? ballot_and(!(v.x >= t0), !(T.x < b0)) : __builtin_amdgcn_ballot_w64(!(v.x >= t0));
         const uint64_t f1m = kBehind ? ballot_and(!(v.y >= t1), !(T.y < b1)) : __builtin_amdgcn_ballot_w64(!(v.y >= t1));
         const bool f0 = f0m != 0, f1 = f1m != 0;
-        uint64_t bw0[W], bw1[W];  // member 0 and 1 bits in word w
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const v4f_t rb = w == 0 ? r2 : e[3 + w];
-            bw0[w] = (uint64_t)__float_as_uint(rb.x) | ((uint64_t)__float_as_uint(rb.y) << 32);
-            bw1[w] = (uint64_t)__float_as_uint(rb.z) | ((uint64_t)__float_as_uint(rb.w) << 32);
-        }
         if constexpr (W == 1) {
-            wave[0] |= (f0 ? bw0[0] : 0ull) | (f1 ? bw1[0] : 0ull);
-        } else {
+            const uint64_t b0 = (uint64_t)__float_as_uint(r2.x) | ((uint64_t)__float_as_uint(r2.y) << 32);
+            const uint64_t b1 = (uint64_t)__float_as_uint(r2.z) | ((uint64_t)__float_as_uint(r2.w) << 32);
+            wave[0] |= (f0 ? b0 : 0ull) | (f1 ? b1 : 0ull);
+        } else if constexpr (W == 2) {
+            uint64_t bw0[W], bw1[W];  // member 0 and 1 bits in word w
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const v4f_t rb = w == 0 ? r2 : e[3 + w];
+                bw0[w] = (uint64_t)__float_as_uint(rb.x) | ((uint64_t)__float_as_uint(rb.y) << 32);
+                bw1[w] = (uint64_t)__float_as_uint(rb.z) | ((uint64_t)__float_as_uint(rb.w) << 32);
+            }
             merge_words<W>(wave, f0m, bw0);
             merge_words<W>(wave, f1m, bw1);
+        } else {
+            // four-word tables: a member's four bit rows are read only when some lane flagged it (a
+            // uniform branch), so they do not hold 16 SGPRs across every entry's prefilter (RTWeekend
+            // +0.7 %; the two-word form keeps its selects: C5 -0.5 % this way, profiles/r05u_lazy_bits_ab.txt)
+            if (f0 | f1) {
+                cv4f_t *eb = opaque(e);
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const v4f_t rb = w == 0 ? eb[2] : eb[3 + w];
+                    if (f0) wave[w] |= (uint64_t)__float_as_uint(rb.x) | ((uint64_t)__float_as_uint(rb.y) << 32);
+                    if (f1) wave[w] |= (uint64_t)__float_as_uint(rb.z) | ((uint64_t)__float_as_uint(rb.w) << 32);
+                }
+            }
         }
     }
 }
