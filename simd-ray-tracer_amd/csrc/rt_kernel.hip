@@ -1072,6 +1072,23 @@ template <int WALK> struct Walk {
     static constexpr bool CLUSTERS = WALK >= kWalkCl1;
 };
 
+// Tile of this block: heaviest-first order from the previous launch's
+// measured costs when the host supplies one (tile_order), so the long
+// waves do not start last and form the launch's tail.  One-wave kernels
+// rank waves (unit 4 * tile + quadrant), four-wave ones block tiles.
+template <bool SOLO, typename Args>
+__device__ __forceinline__ void wave_unit(const Args &a, uint32_t tid, uint32_t &tile, uint32_t &wave) {
+    if (SOLO && a.unit_waves != 0u) {
+        const uint32_t u = a.tile_order ? a.tile_order[blockIdx.x] : blockIdx.x;
+        tile = u >> 2;
+        wave = u & 3u;
+    } else {
+        const uint32_t blk = SOLO ? blockIdx.x >> 2 : blockIdx.x;
+        tile = a.tile_order ? a.tile_order[blk] : blk;
+        wave = SOLO ? blockIdx.x & 3u : tid >> 6;
+    }
+}
+
 template <bool SIMD, int SRC, bool CULL, int P, bool GS, bool SOLO = false, int WALK = kWalkAny>
 __global__ __launch_bounds__(SOLO ? 64 : 256, SOLO ? solo_waves(WALK) : SRC == kSrcSmem ? RTK_MIN_WAVES_PER_SIMD : 1)
 void trace_kernel(TraceArgs a) {
@@ -1125,24 +1142,16 @@ void trace_kernel(TraceArgs a) {
     // wave: quadrant of the block tile; sw: the wave's LDS slot in its workgroup
     const uint32_t tid = threadIdx.x, lane = tid & 63u;
     const uint32_t sw = SOLO ? 0u : tid >> 6;
-    const uint64_t t_start = a.wave_times ? __builtin_amdgcn_s_memrealtime() : 0;
-    // Tile of this block: heaviest-first order from the previous launch's
-    // measured costs when the host supplies one (tile_order), so the long
-    // waves do not start last and form the launch's tail.  One-wave kernels
-    // rank waves (unit 4 * tile + quadrant), four-wave ones block tiles.
     uint32_t tile, wave;
-    const bool unit_waves = SOLO && a.unit_waves != 0u;
-    if (unit_waves) {
-        const uint32_t u = a.tile_order ? a.tile_order[blockIdx.x] : blockIdx.x;
-        tile = u >> 2;
-        wave = u & 3u;
-    } else {
-        const uint32_t blk = SOLO ? blockIdx.x >> 2 : blockIdx.x;
-        tile = a.tile_order ? a.tile_order[blk] : blk;
-        wave = SOLO ? blockIdx.x & 3u : tid >> 6;
-    }
+    wave_unit<SOLO>(a, tid, tile, wave);
     const uint32_t tile_x = tile % a.tiles_x, tile_y = tile / a.tiles_x;
-    const uint64_t t_cost0 = a.tile_cost ? __builtin_amdgcn_s_memtime() : 0;
+    // The wave's start times go to memory and LDS, and the end of the kernel re-derives its tile
+    // (wave_unit through the kernarg segment): nothing of the bookkeeping is held in SGPRs across the
+    // trip loop, where the four-word walk spilled it around every secondary round.
+    __shared__ uint64_t s_cost0[SOLO ? 1 : kWB];
+    if (a.wave_times && lane == 0) a.wave_times[2u * ((uint64_t)tile * 4u + wave)] = __builtin_amdgcn_s_memrealtime();
+    if (a.tile_cost && lane == 0) s_cost0[sw] = __builtin_amdgcn_s_memtime();
+    const uint64_t t_cost0 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t pl = lane / LP, j = lane % LP;  // pixel of the tile, sample lane of the pixel
     // wave tile: a TW x TH quadrant of the block tile, or (interleave) every
     // other pixel and row of the whole block tile, parity (wave & 1, wave >> 1);
@@ -1648,24 +1657,25 @@ void trace_kernel(TraceArgs a) {
     }
     if (Q == 1 && valid && owner && a.frames > 0) store_pixel();  // (Q > 1: stored as each pixel completes)
 
-    if (a.pix_cost) {  // the pixel's traced segments over its P lanes (every lane active here)
+    cargs_t &ka = kernel_args();  // (the end's fields from the kernarg segment: see wave_unit above)
+    if (ka.pix_cost) {  // the pixel's traced segments over its P lanes (every lane active here)
         for (uint32_t off = 1; off < LP; off <<= 1) pseg += (uint32_t)__shfl_xor((int)pseg, (int)off, 64);
-        if (Q == 1 && valid && owner) a.pix_cost[(size_t)ly * a.width + x] = pseg;
+        if (Q == 1 && valid && owner) ka.pix_cost[(size_t)ly * ka.width + x] = pseg;
     }
     // ---- ray counter (RaysCastInThread, main.cpp:390): one atomic per wave
-    if (lane == 0 && nrays) atomicAdd(a.rays, (unsigned long long)nrays);
-    if (a.tile_cost && lane == 0) {
-        const uint64_t c = __builtin_amdgcn_s_memtime() - t_cost0;
-        const uint32_t c32 = (uint32_t)(c < 0xFFFFFFFFull ? c : 0xFFFFFFFFull);
-        if (unit_waves)
-            a.tile_cost[4u * tile + wave] = c32 | 1u;  // (>= 1: a launched wave never ranks with dead ones)
-        else
-            atomicMax(a.tile_cost + tile, c32);
-    }
-    if (a.wave_times && lane == 0) {
-        const uint64_t wid = (uint64_t)tile * 4u + wave;
-        a.wave_times[2 * wid + 0] = t_start;
-        a.wave_times[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && nrays) atomicAdd(ka.rays, (unsigned long long)nrays);
+    if ((ka.tile_cost || ka.wave_times) && lane == 0) {
+        uint32_t tile_e, wave_e;
+        wave_unit<SOLO>(ka, tid, tile_e, wave_e);
+        if (ka.tile_cost) {
+            const uint64_t c = __builtin_amdgcn_s_memtime() - s_cost0[sw];
+            const uint32_t c32 = (uint32_t)(c < 0xFFFFFFFFull ? c : 0xFFFFFFFFull);
+            if (SOLO && ka.unit_waves != 0u)
+                ka.tile_cost[4u * tile_e + wave_e] = c32 | 1u;  // (>= 1: a launched wave never ranks with dead ones)
+            else
+                atomicMax(ka.tile_cost + tile_e, c32);
+        }
+        if (ka.wave_times) ka.wave_times[2u * ((uint64_t)tile_e * 4u + wave_e) + 1u] = __builtin_amdgcn_s_memrealtime();
     }
     if (kStats && a.stats && lane == 0) {
         atomicAdd(a.stats + kStatPriIters, (unsigned long long)st_pri_it);
