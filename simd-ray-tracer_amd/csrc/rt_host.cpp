@@ -323,7 +323,7 @@ extern "C" int rt_set_rsqrt_table(rt_device *d, const float table[2048]) {
 }
 
 // Packs one rule set: positions/radii as 4-wide groups with r*r precomputed,
-// materials as {Color.xyz, Specular}, {Emissive.xyz, IOR}.
+// sphere records as {centre.xyz, 0}, {Color.xyz, Specular}, {Emissive.xyz, IOR}, {0} (kSphereF4).
 static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, const std::vector<float> &mats,
                       uint32_t n_groups) {
     if (n_groups > d->cap_groups[rs]) {
@@ -335,7 +335,7 @@ static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, co
         d->d_prim[rs] = nullptr;
         // +2 padding groups: the kernel's loops prefetch up to group g+2 while testing g
         if (hipMalloc(&d->d_groups[rs], (size_t)(n_groups + 2) * kGroupF4 * 16) != hipSuccess ||
-            hipMalloc(&d->d_mats[rs], (size_t)n_groups * 128) != hipSuccess ||
+            hipMalloc(&d->d_mats[rs], (size_t)n_groups * 64u * kSphereF4) != hipSuccess ||
             hipMalloc(&d->d_prim[rs], (size_t)n_groups * kPrimF4 * 16) != hipSuccess)
             return fail(RT_ENOMEM, "rt_scene_upload: device allocation failed");
         d->cap_groups[rs] = n_groups;
@@ -343,7 +343,8 @@ static int upload_set(rt_device *d, int rs, const std::vector<float> &groups, co
     HIP_OK(hipMemsetAsync(d->d_groups[rs] + kGroupF4 * (size_t)n_groups, 0, 2 * kGroupF4 * 16, d->stream));
     HIP_OK(hipMemcpyAsync(d->d_groups[rs], groups.data(), (size_t)n_groups * kGroupF4 * 16, hipMemcpyHostToDevice,
                           d->stream));
-    HIP_OK(hipMemcpyAsync(d->d_mats[rs], mats.data(), (size_t)n_groups * 128, hipMemcpyHostToDevice, d->stream));
+    HIP_OK(hipMemcpyAsync(d->d_mats[rs], mats.data(), (size_t)n_groups * 64u * kSphereF4, hipMemcpyHostToDevice,
+                          d->stream));
     d->n_groups[rs] = n_groups;
     return RT_OK;
 }
@@ -829,7 +830,7 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
     const uint32_t n = rs == 0 ? ng : ngs;
     p.n_groups = n;
     p.groups.assign((size_t)n * 4 * kGroupF4, 0.0f);
-    p.mats.assign((size_t)n * 32, 0.0f);
+    p.mats.assign((size_t)n * 16u * kSphereF4, 0.0f);  // sphere records (rt_kernel.h kSphereF4)
     std::vector<float> &gv = p.groups;
     if (rs == 0) {
         const rt_sphere_group *g = (const rt_sphere_group *)scene->SIMDSpheres.Data;
@@ -841,7 +842,11 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
                 gv[i * 4 * kGroupF4 + 4 * kRowZ + l] = g[i].Z[l];
                 gv[i * 4 * kGroupF4 + 4 * kRowR2 + l] = g[i].Radii[l] * g[i].Radii[l];
                 const uint32_t s = 4u * i + (uint32_t)l;
-                if (s < scene->Materials.Count) put_material(&p.mats[(size_t)s * 8], m[s]);
+                float *rec = &p.mats[(size_t)s * 4u * kSphereF4];
+                rec[0] = g[i].X[l];
+                rec[1] = g[i].Y[l];
+                rec[2] = g[i].Z[l];
+                if (s < scene->Materials.Count) put_material(rec + 4, m[s]);
             }
         }
     } else {
@@ -852,7 +857,11 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
             gv[gi * 4 * kGroupF4 + 4 * kRowY + l] = s[i].Position.y;
             gv[gi * 4 * kGroupF4 + 4 * kRowZ + l] = s[i].Position.z;
             gv[gi * 4 * kGroupF4 + 4 * kRowR2 + l] = s[i].Radius * s[i].Radius;
-            put_material(&p.mats[(size_t)i * 8], s[i].Material);
+            float *rec = &p.mats[(size_t)i * 4u * kSphereF4];
+            rec[0] = s[i].Position.x;
+            rec[1] = s[i].Position.y;
+            rec[2] = s[i].Position.z;
+            put_material(rec + 4, s[i].Material);
         }
         for (uint32_t i = ns; i < ngs * 4u; ++i) gv[(i / 4u) * 4 * kGroupF4 + 4 * kRowR2 + (i % 4u)] = -__builtin_inff();
     }

@@ -10,6 +10,7 @@ constexpr uint32_t kGroupF4 = 5;      // float4 rows per sphere group:
 constexpr uint32_t kRowX = 0, kRowY = 1, kRowZ = 2;  //   centres
 constexpr uint32_t kRowR2P = 3;       //   prefilter thresholds (rows 0-3 = one s_load_dwordx16)
 constexpr uint32_t kRowR2 = 4;        //   r*r
+constexpr uint32_t kSphereF4 = 4;     // float4 rows per sphere record (TraceArgs.materials)
 enum { kFlagAccumZero = 1, kFlagSrgbPow = 2 };
 // Clustered secondary-ray prefilter (rt_host.cpp cluster_table): entries of
 // cl_entry_f4(W) float4 rows, read through the scalar cache --
@@ -42,7 +43,9 @@ constexpr uint32_t kClAutoGroups = 128;  // used by default up to this many (rt_
 //   groups    : n_groups x 5 float4 = {x[4]}, {y[4]}, {z[4]}, {r2p[4]}, {r*r[4]}  (80 B/group)
 //               r2p = prefilter threshold of the secondary-ray sphere loop (rt_host.cpp);
 //               with pf_relative, r*r again (-inf: never hit) and the threshold is formed per lane
-//   materials : 4*n_groups x 2 float4 = {Color.xyz, Specular}, {Emissive.xyz, IOR} (32 B/sphere)
+//   spheres   : 4*n_groups records of kSphereF4 float4 = {centre.xyz, 0}, {Color.xyz, Specular},
+//               {Emissive.xyz, IOR}, {0} (64 B/sphere: what shading gathers for the winning sphere,
+//               addressed by one shift of its index; TraceArgs.materials)
 // r*r is precomputed on the host with the same f32 multiply the reference
 // repeats per test (main.cpp:406), so it is bit-identical.
 struct TraceArgs {
@@ -137,7 +140,9 @@ constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 // weights are then two divisions per sample): C5 fits 7 blocks per CU.
 static inline bool rtk_lut_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
 static inline bool rtk_fold_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
-static inline size_t rtk_scene_lds_bytes(uint32_t n_groups) { return (size_t)n_groups * (16u * kGroupF4 + 128u); }
+static inline size_t rtk_scene_lds_bytes(uint32_t n_groups) {
+    return (size_t)n_groups * (16u * kGroupF4 + 64u * kSphereF4);
+}
 static inline size_t rtk_lds_bytes(const TraceArgs *a) {
     return (a->lut_in_lds ? 8192u : 0u) + (a->fold_in_lds ? 2048u : 0u) +
            (a->scene_in_lds ? rtk_scene_lds_bytes(a->n_groups) : 0u);
@@ -147,7 +152,7 @@ static inline size_t rtk_lds_bytes(const TraceArgs *a) {
 // (scene_in_lds = 0): the sphere loop reads groups through the scalar cache as
 // always, and the per-lane gathers go through L1/L2.  Up to kMaxGroups groups
 // (the primary cull masks are kMaxGroups / 64 words per wave tile).
-static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4 + 128u);  // 265 groups
+static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4 + 64u * kSphereF4);  // 164 groups
 static const uint32_t kMaxGroups = 4096u;                                                    // 16,384 spheres
 
 extern "C" int rtk_launch_trace(const TraceArgs *a, int simd, int src, int cull, int lanes_per_pixel,

@@ -1105,7 +1105,7 @@ void trace_kernel(TraceArgs a) {
     if (a.live_total && (SOLO ? blockIdx.x >> 2 : blockIdx.x) >= (uint32_t)*a.live_total) return;
     const uint64_t st_entry = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     // LDS image: [rsqrt table 512 float4][fold table 128 float4]
-    //            [groups 4*n_groups float4][materials 8*n_groups float4]
+    //            [groups kGroupF4*n_groups float4][sphere records kSphereF4*4*n_groups float4]
     // the wave tile's primary group mask: one-wave workgroups keep no LDS image,
     // so theirs is the dynamic LDS the host sizes to the scene's words (static
     // kMaxGroups / 64 words would cost 512 B of every workgroup's allocation)
@@ -1123,14 +1123,13 @@ void trace_kernel(TraceArgs a) {
     float4 *lds_groups = smem + lut_f4 + fold_n / 2;
     float4 *lds_mats = lds_groups + kGroupF4 * a.n_groups;
     // per-lane gathers of the winner's centre and material: LDS image or HBM (GS)
-    const float *sph_src = GS ? reinterpret_cast<const float *>(a.groups) : reinterpret_cast<const float *>(lds_groups);
     const float4 *mat_src = GS ? a.materials : lds_mats;
     {
         const float4 *glut = reinterpret_cast<const float4 *>(a.rsqrt_lut);
         for (uint32_t i = threadIdx.x; i < lut_f4; i += blockDim.x) smem[i] = glut[i];
         if (!GS) {
             for (uint32_t i = threadIdx.x; i < kGroupF4 * a.n_groups; i += blockDim.x) lds_groups[i] = a.groups[i];
-            for (uint32_t i = threadIdx.x; i < 8u * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
+            for (uint32_t i = threadIdx.x; i < 4u * kSphereF4 * a.n_groups; i += blockDim.x) lds_mats[i] = a.materials[i];
         }
         // running-mean weights of frame k (main.cpp:484-487): 1/(p+1), p/(p+1)
         for (uint32_t i = threadIdx.x; i < fold_n; i += blockDim.x) {
@@ -1325,16 +1324,19 @@ void trace_kernel(TraceArgs a) {
     // Re-derive the winner's HitNormal / NextRayOrigin exactly as they were
     // formed at acceptance (main.cpp:423-429), then shade and bounce.
     auto shade_hit = [&](float tmin, uint32_t sidx, bool inside) {
-        const float *gsph = sph_src + 4u * kGroupF4 * (sidx >> 2) + (sidx & 3u);
-        const float sx = gsph[0], sy = gsph[4], sz = gsph[8];
+        // the winner's record (rt_kernel.h kSphereF4): one shift of the sphere index addresses its
+        // centre and both material rows
+        const float4 *rec = mat_src + kSphereF4 * sidx;
+        const float4 sc = rec[0];
+        const float sx = sc.x, sy = sc.y, sz = sc.z;
         const float cx = sx - p.rx.x, cy = sy - p.ry.x, cz = sz - p.rz.x;
         const float ipx = p.rx.y * tmin, ipy = p.ry.y * tmin, ipz = p.rz.y * tmin;
         const float hx = ipx - cx, hy = ipy - cy, hz = ipz - cz;
         p.rx.x = p.rx.x + ipx;
         p.ry.x = p.ry.x + ipy;
         p.rz.x = p.rz.x + ipz;
-        const float4 cs = mat_src[2u * sidx + 0u];
-        const float4 ei = mat_src[2u * sidx + 1u];
+        const float4 cs = rec[1];
+        const float4 ei = rec[2];
         shade(lut, cs, ei, hx, hy, hz, inside, p);
         if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
         p.bounce += 1;

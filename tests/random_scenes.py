@@ -4,7 +4,7 @@ The kernel skips work by proofs that rest on host-derived error bounds: the
 f64 primary-ray cone cull, the FMA secondary-ray prefilter, the cluster walk
 and its behind-origin rule.  The built-in scenes exercise them
 only in one regime, so this generator builds scenes that stress the slack:
-- sphere counts from 1 to 1,060 (265 groups, the LDS-staged maximum);
+- sphere counts from 1 to 1,060 (265 groups; the four-wave kernels' LDS image holds up to 164);
 - radii log-uniform over 1e-3 ... 1e2 of a world scale itself drawn from
   1e-2 ... 1e2 (so the reference's absolute eps = 1e-4 is met at every scale),
   or, in "cloud" scenes, within one decade (the scene-wide prefilter bound

@@ -146,7 +146,7 @@ def test_trace_rejects_bad_arguments(rt):
 def test_scene_size_limits(rt):
     """rt_scene_upload's packer (shared with rt_scene_prefilter, no GPU needed)
     rejects an empty scene and one past RT_MAX_SPHERES; scenes past the LDS
-    image's 1,060 spheres are accepted (they stay in HBM)."""
+    image's 656 spheres (164 groups) are accepted (they stay in HBM)."""
     empty = rt.scene_from_spheres(np.zeros((0, 20), np.float32), use_sky=True)
     with pytest.raises(rt.RtError, match="empty scene"):
         rt.scene_prefilter(empty, True)
@@ -155,8 +155,8 @@ def test_scene_size_limits(rt):
     sp[:, 4] = 0.25
     with pytest.raises(rt.RtError, match="exceed the limit"):
         rt.scene_prefilter(rt.scene_from_spheres(sp[:]), True)
-    r2, _, _ = rt.scene_prefilter(rt.scene_from_spheres(sp[:4 * 265 + 1]), True)  # one past the LDS image
-    assert len(r2) == 4 * 266
+    r2, _, _ = rt.scene_prefilter(rt.scene_from_spheres(sp[:4 * 164 + 1]), True)  # one past the LDS image
+    assert len(r2) == 4 * 165
 
 
 def test_frame_hash_is_the_fixtures_fnv1a(rt, orc):

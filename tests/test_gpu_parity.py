@@ -667,31 +667,40 @@ def test_encode_rgba8_exhaustive(rt, orc, torch_cuda):
         assert np.array_equal(got, want), f"pow={pw}: {int((got != want).sum())} pixels differ"
 
 
-def test_largest_scene_the_lds_image_holds(rt, orc, torch_cuda, gdev):
-    """1,060 spheres = 265 groups, the LDS-staged maximum (rt_kernel.h
-    kMaxLdsGroups): RTWeekend's 482 plus small spheres scattered over its
-    ground (their materials copied from RTWeekend's), both rule sets."""
+@pytest.mark.parametrize("n_groups", [164, 265])
+def test_largest_scene_the_lds_image_holds(rt, orc, torch_cuda, gdev, monkeypatch, n_groups):
+    """164 groups (656 spheres) is the LDS-staged maximum of the four-wave
+    kernels (rt_kernel.h kMaxLdsGroups, 64-B sphere records); 265 groups stay
+    in HBM.  RTWeekend's 482 spheres plus (or, at 164 groups, minus) small
+    spheres scattered over its ground (materials copied from RTWeekend's),
+    both rule sets, traced by the four-wave kernels that stage the image."""
+    monkeypatch.setenv("RT_SOLO", "0")
+    gdev = rt.Device(0)
     base = rt.scene_builtin(2)
     sp0, _, _ = rt.scene_arrays(base)
     rng = np.random.default_rng(265)
-    extra = sp0[rng.integers(1, len(sp0), 4 * 265 - len(sp0))].copy()
+    n = 4 * n_groups
+    extra = sp0[rng.integers(1, len(sp0), max(n - len(sp0), 0))].copy()
     extra[:, 0] = rng.uniform(-1.5, 1.5, len(extra))  # the scene is at 1/16 scale
     extra[:, 2] = rng.uniform(-1.5, 1.5, len(extra))
     extra[:, 4] = rng.uniform(0.005, 0.02, len(extra))
     extra[:, 1] = extra[:, 4]
-    sp = np.concatenate([sp0, extra]).astype(np.float32)
+    sp = np.concatenate([sp0, extra]).astype(np.float32)[:n]
     la = (base.LookAt.x, base.LookAt.y, base.LookAt.z)
     kw = dict(distance=base.DefaultDistanceFromLookAt, x_angle=base.DefaultXAngle, y_height=base.DefaultYHeight)
     s = rt.scene_from_spheres(sp, look_at=la, use_sky=True, **kw)
     _, groups, mats = rt.scene_arrays(s)
-    assert len(groups) == 265
+    assert len(groups) == n_groups
     o = orc.Scene(sp, groups, mats, look_at=la, use_sky=True, **kw)
     W, H = 48, 32
     cam = rt.camera_setup(s, W, H)
-    for simd in (True, False):
-        g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5, simd=simd)
-        r = orc.render(o, orc.camera(o, W, H), W, H, frames=2, max_bounce=5, simd=simd)
-        assert_same(*g, *r)
+    try:
+        for simd in (True, False):
+            g = gpu_render(rt, torch_cuda, gdev, s, cam, W, H, frames=2, bounces=5, simd=simd)
+            r = orc.render(o, orc.camera(o, W, H), W, H, frames=2, max_bounce=5, simd=simd)
+            assert_same(*g, *r)
+    finally:
+        gdev.close()
 
 
 def test_upload_waits_for_traces_in_flight(rt, orc, torch_cuda):
@@ -738,7 +747,8 @@ def test_upload_waits_for_traces_in_flight(rt, orc, torch_cuda):
 
 @pytest.mark.parametrize("n_spheres", [1061, 2000, 4099])
 def test_scene_beyond_the_lds_image(rt, orc, torch_cuda, gdev, n_spheres):
-    """Scenes above 1,060 spheres (265 groups) stay in HBM: the sphere loop
+    """Scenes above 656 spheres (164 groups) stay in HBM even for the four-wave
+    kernels (the one-wave default keeps every scene there): the sphere loop
     reads groups through the scalar cache and the winner / material / r^2
     gathers go through the caches.  RTWeekend's 482 spheres plus small spheres
     scattered over its ground, both rule sets, bit-exact against the oracle."""
