@@ -1115,11 +1115,14 @@ void trace_kernel(TraceArgs a) {
     // pixel (different slots) fall on different LDS banks (stride NPIX + 1)
     constexpr uint32_t kRingStride = NPIX + 1u;
     __shared__ float4 s_ring[LP > 1 ? kWB * kRing * kRingStride : 1];
-    const uint32_t lut_f4 = a.lut_in_lds ? 512u : 0u;  // see rtk_lds_bytes
-    const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, a.lut_in_lds != 0u};
+    // (one-wave kernels keep no LDS image: both tables are theirs from HBM at compile time, so the
+    // rsqrt gather is a global load with a scalar base, not a flat one through a selected pointer)
+    const bool lut_lds = !SOLO && a.lut_in_lds != 0u;
+    const uint32_t lut_f4 = lut_lds ? 512u : 0u;  // see rtk_lds_bytes
+    const Lut lut = {reinterpret_cast<const float *>(smem), a.rsqrt_lut, lut_lds};
     float2 *fold = reinterpret_cast<float2 *>(smem + lut_f4);
     // running-mean weights of the first kFoldTable frames (large scenes: none, computed per sample)
-    const uint32_t fold_n = a.fold_in_lds ? kFoldTable : 0u;
+    const uint32_t fold_n = !SOLO && a.fold_in_lds ? kFoldTable : 0u;
     float4 *lds_groups = smem + lut_f4 + fold_n / 2;
     float4 *lds_mats = lds_groups + kGroupF4 * a.n_groups;
     // per-lane gathers of the winner's centre and material: LDS image or HBM (GS)
