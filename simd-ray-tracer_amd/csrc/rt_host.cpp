@@ -20,6 +20,7 @@ struct rt_device {
     bool lut_set = false;
     // SIMD rule set (SIMDSpheres + Materials) and scalar rule set (ScalarSpheres)
     float4 *d_groups[2] = {nullptr, nullptr};
+    float2 *d_weights = nullptr;  // TraceArgs.weights: kWeightsN running-mean weight pairs
     // the primary rounds' camera-relative group rows (TraceArgs.prim), written by the cull pass
     float4 *d_prim[2] = {nullptr, nullptr};
     float4 *d_mats[2] = {nullptr, nullptr};
@@ -172,10 +173,24 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
     d->ordinal = hip_device;
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&d->d_lut, 2048 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&d->d_weights, kWeightsN * sizeof(float2)) != hipSuccess ||
         hipHostMalloc(&d->h_counts, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_counts, hipEventDisableTiming) != hipSuccess) {
         rt_device_destroy(d);
         return fail(RT_ENOMEM, "rt_device_create: stream/LUT/event allocation failed");
+    }
+    {
+        // IEEE f32 divisions (this file is built with -ffp-contract=off): the bits of the kernel's
+        // rcp_rn / div_rn weights, which reproduce the reference's divisions (main.cpp:484-487)
+        std::vector<float2> w(kWeightsN);
+        for (uint32_t n = 0; n < kWeightsN; ++n) {
+            const float d1 = (float)(n + 1u);
+            w[n] = make_float2(1.0f / d1, (float)n / d1);
+        }
+        if (hipMemcpy(d->d_weights, w.data(), kWeightsN * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+            rt_device_destroy(d);
+            return fail(RT_EIO, "rt_device_create: weight table upload failed");
+        }
     }
     {
         hipDeviceProp_t prop;
@@ -257,6 +272,7 @@ extern "C" int rt_device_destroy(rt_device *d) {
         (void)hipFree(d->d_clusters[r]);
     }
     (void)hipFree(d->d_lut);
+    (void)hipFree(d->d_weights);
     (void)hipFree(d->d_stats);
     (void)hipFree(d->d_wave_times);
     (void)hipFree(d->d_tile_cost);
@@ -1102,6 +1118,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     a.groups = d->d_groups[rs];
     a.materials = d->d_mats[rs];
     a.rsqrt_lut = d->d_lut;
+    a.weights = d->d_weights;
     a.prev = (float4 *)cam->PreviousImage.Data;
     a.cur = (uint32_t *)cam->CurrentImage.Data;
     a.rays = (unsigned long long *)d_rays;

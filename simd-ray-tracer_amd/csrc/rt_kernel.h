@@ -112,7 +112,12 @@ struct TraceArgs {
     // c = RN(centre - CameraPosition), the first three f32 ops of every primary sphere test
     // (main.cpp:401), identical on every lane of a primary round (one s_load_dwordx16)
     float4 *prim;
+    // the running-mean weights {RN(1/(n+1)), RN(n/(n+1))} of frames n < kWeightsN (main.cpp:484-487),
+    // one table per device computed once (rt_device_create): a finished sample's two weights are one
+    // gather instead of two conversions, a reciprocal and a division (one-wave kernels)
+    const float2 *weights;
 };
+constexpr uint32_t kWeightsN = 65536;
 constexpr uint32_t kPrimF4 = 4;
 constexpr uint32_t kMergeGroups = 2;
 // Cull pass counters (rtk_launch_cull): [0, 64) striped live block tiles, [64, 128)

@@ -1612,7 +1612,9 @@ void trace_kernel(TraceArgs a) {
                     const float oz = a.max_bounce == 0 ? 0.0f : p.cz;
                     if (LP == 1) {
                         // ---- running-mean blend (main.cpp:484-489), in order by construction
-                        const float2 fw = k < fold_n ? fold[k] : fold_weights(a.prev_count + k);
+                        const uint32_t pc = a.prev_count + k;
+                        const float2 fw = SOLO ? (pc < kWeightsN ? a.weights[pc] : fold_weights(pc))
+                                               : k < fold_n ? fold[k] : fold_weights(pc);
                         const float inv = fw.x, ratio = fw.y;
                         accx = ox * inv + accx * ratio;
                         accy = oy * inv + accy * ratio;
@@ -1621,8 +1623,14 @@ void trace_kernel(TraceArgs a) {
                     } else {
                         // park Out*(1/n) and the ratio (n-1)/n of sample k's blend; the
                         // sign bit of .w marks the slot ready (the ratio is >= 0)
-                        float2 w = fold[k < fold_n ? k : 0u];  // (fold_n = 0: an unused in-bounds read)
-                        if (__builtin_expect(k >= fold_n, 0)) w = fold_weights(a.prev_count + k);
+                        float2 w;
+                        if (SOLO) {  // the static table of the first kWeightsN frames (TraceArgs.weights)
+                            const uint32_t pc = a.prev_count + k;
+                            w = pc < kWeightsN ? a.weights[pc] : fold_weights(pc);
+                        } else {
+                            w = fold[k < fold_n ? k : 0u];  // (fold_n = 0: an unused in-bounds read)
+                            if (__builtin_expect(k >= fold_n, 0)) w = fold_weights(a.prev_count + k);
+                        }
                         ring[(k % kRing) * kRingStride] = make_float4(ox * w.x, oy * w.x, oz * w.x, -w.y);
                     }
                     k += kDynamic ? 0u : LP;

@@ -507,13 +507,15 @@ def test_dead_tiles_fold_a_nonzero_running_mean(rt, orc, torch_cuda, gdev):
     assert_same(*g, *r)
 
 
-@pytest.mark.parametrize("prev_count,P", [(1000003, 4), (16777217, 16), (300000001, 1), (4294967000, 8)])
+@pytest.mark.parametrize("prev_count,P", [(65533, 4), (65530, 16), (1000003, 4), (16777217, 16), (300000001, 1),
+                                          (4294967000, 8)])
 def test_running_mean_weights_at_large_previous_counts(rt, orc, torch_cuda, monkeypatch, prev_count, P):
     """The fold weights RN(1/(f32)(n)) and RN((f32)(n-1)/(f32)(n)) (main.cpp:484-487)
-    come from rcp_rn / div_rn (rt_kernel.hip fold_weights) in the one-wave kernels:
-    frames far past the 256-entry weight table, including counts whose f32 conversion
-    rounds (> 2^24) and the top of the u32 range, against the oracle's IEEE divisions,
-    with a random non-zero running mean, every lane shape's blend path."""
+    come from the device's static table of the first 65,536 frames (TraceArgs.weights)
+    and past it from rcp_rn / div_rn (rt_kernel.hip fold_weights) in the one-wave
+    kernels: launches across the table's end, frames far past it, counts whose f32
+    conversion rounds (> 2^24) and the top of the u32 range, against the oracle's IEEE
+    divisions, with a random non-zero running mean, every lane shape's blend path."""
     monkeypatch.setenv("RT_LANES_PER_PIXEL", str(P))
     s, o = _scenes(rt, orc, 1, 64)
     W, H = 64, 48
