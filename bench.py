@@ -233,11 +233,14 @@ def cpu_model() -> str:
 def pmc_record(workload: str, bands: int = 1):
     """The newest committed rocprofv3 --pmc record of this workload and band
     split (profiles/rNN_*_pmc.json, written by scripts/pmc_to_json.py; a
-    record without "bands" is a whole-frame, one-GPU one)."""
+    record without "bands" is a whole-frame, one-GPU one; one marked
+    "superseded_by" was followed by a later kernel's record in the same round)."""
     for f in sorted((ROOT / "profiles").glob("r*_pmc.json"), reverse=True):
         try:
             rec = json.loads(f.read_text())
         except (OSError, ValueError):
+            continue
+        if rec.get("superseded_by"):  # a later kernel's record of the same round exists
             continue
         if rec.get("workload") == workload and int(rec.get("bands", 1)) == bands:
             rec["file"] = f"profiles/{f.name}"
