@@ -166,9 +166,10 @@ int rt_rsqrt_table_capture_host(float table_out[2048]);
 
 /* Uploads Scenes[SceneIndex] (read by RenderTile at main.cpp:370) into
  * HBM: SIMDSpheres/Materials for the SIMD rules, ScalarSpheres for the
- * scalar rules.  The scene is copied; the caller keeps ownership.  Scenes
- * up to 1,060 spheres (265 groups) are also staged in each block's LDS; larger
- * ones, up to RT_MAX_SPHERES, are read from HBM through the caches.
+ * scalar rules.  The scene is copied; the caller keeps ownership.  The
+ * default one-wave kernels read every scene from HBM through the caches; the
+ * four-wave kernels (RT_SOLO=0) also stage scenes of up to 656 spheres (164
+ * groups) in each block's LDS.  Up to RT_MAX_SPHERES.
  * RT_EINVAL for a scene with no spheres (every built-in scene has some) or
  * more than RT_MAX_SPHERES. */
 #define RT_MAX_SPHERES 16384u
