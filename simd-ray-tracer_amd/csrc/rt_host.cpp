@@ -68,7 +68,11 @@ struct rt_device {
     uint32_t pixel_seg = 1;
     // RT_XCD_GROUP: every wave of a block tile on one XCD (rtk_launch_xcd_group), so its lines'
     // partial stores merge in one L2 before they are written back
-    int xcd_group_env = 1;
+    // RT_XCD_GROUP=0/1 forces it off/on; by default it is on for launches of at most 4 lanes per pixel (the
+    // whole frame, where it halves the trace kernel's HBM writes at no cost) and off for the multi-GPU shares
+    // (8 and 16 lanes per pixel: small launches, whose partial-line writes are a few MB, and the 8-rank share
+    // -2.3 % without it at the final kernel, profiles/r05z6_xcd_group_ab.txt)
+    int xcd_group_env = -1;
     // RGBA8 encoded from the running mean by a coalesced pass after the launch (TraceArgs.skip_cur),
     // at P >= 2: trace-kernel HBM writes C2 21.0 -> 15.7 MB, RTWeekend 80.6 -> 54.1 MB, C2 +0.7 %
     // (profiles/r05e_cur_pass_ab.txt); RT_CUR_PASS=0 stores RGBA8 in the trace kernel
@@ -1386,7 +1390,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
         if (resort) {
             d->n_sorts += 1;
             // one-wave kernels: sort, then group each block tile's waves onto one XCD
-            const bool group = a.unit_waves && d->xcd_group_env;
+            const bool group = a.unit_waves && (d->xcd_group_env == 1 || (d->xcd_group_env < 0 && lpp <= 4));
             if (rtk_launch_tile_sort(d->d_tile_cost, group ? d->d_tile_order_sorted : d->d_tile_order,
                                      d->d_tile_scratch, n_units, s) != 0 ||
                 (group && rtk_launch_xcd_group(d->d_tile_order_sorted, d->d_tile_order, n_units,
