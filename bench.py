@@ -91,6 +91,16 @@ def parse():
     p.add_argument("--modes", default="static,moving", help="onrender: camera modes to run (static, moving)")
     p.add_argument("--no-register", action="store_true",
                    help="onrender: hand frames out through the library's staging buffer (no registered image)")
+    p.add_argument("--opt", action="append", default=[], metavar="FIELD=VALUE",
+                   help="rt_device_options field for every device (include/rt_trace.h), e.g. --opt XcdGroup=off "
+                        "--opt LanesPerPixel=16; switches take on/off/default.  A/B experiments only: every "
+                        "option gives the same bits")
+    p.add_argument("--brute", action="store_true",
+                   help="time the brute-force kernel (Cull=off, Prefilter=off: every counted segment tests every "
+                        "sphere, main.cpp:399-430) as the main line; its roofline is SURVEY 8d's algorithmic one")
+    p.add_argument("--headline-only", action="store_true",
+                   help="skip the extra legs after the timed steps (the brute-force roofline leg and the "
+                        "distinct-samples leg): the PMC passes and kernel traces record the headline launches only")
     a = p.parse_args()
     if a.config == "onrender":
         return a
@@ -98,6 +108,17 @@ def parse():
         if getattr(a, k) is None:
             setattr(a, k, v)
     return a
+
+
+def device_options(rt, args) -> dict:
+    """The rt_device_options of this run (--opt, --brute); {} = the library's defaults."""
+    opts = rt.parse_options(args.opt)
+    if args.brute:
+        opts.update(Cull=rt.RT_OPT_OFF, Prefilter=rt.RT_OPT_OFF)
+    return {k: v for k, v in opts.items() if v}
+
+
+BRUTE = {"Cull": -1, "Prefilter": -1}  # rt_device_options of the brute-force kernel (RT_OPT_OFF)
 
 
 def make_scene(rt, args):
@@ -128,12 +149,53 @@ def golden_for(args, W, H, S, N, B):
     return None, None
 
 
+ROWS_GOLDEN = ROOT / "tests" / "golden" / "c5_rows.json"
+
+
+def rows_golden_for(args, W, H, S, N, B):
+    """The committed tile-row fixture of this workload (tests/golden/c5_rows.json:
+    whole 32-row tile rows of C5 rendered by the reference's own RenderTile and
+    by the oracle, tests/golden/make_c5_rows.py), or None."""
+    try:
+        g = json.loads(ROWS_GOLDEN.read_text())
+    except (OSError, ValueError):
+        return None
+    if (g["scene"] == args.scene and g["width"] == W and g["height"] == H and g["frames"] == S
+            and g["bounces"] == B and g["spheres"] == N and g["simd"] == (not args.scalar) and args.distance is None):
+        return g
+    return None
+
+
+def check_rows(rt, g, W, cur_host, prev_host):
+    """A whole frame too large for a CPU render (C5): its fixture's tile rows, hashed."""
+    got, ok = {}, True
+    for ty, e in g["tile_rows"].items():
+        y0, y1 = e["rows"]
+        h = {"rgba8": f"{rt.frame_hash(cur_host[y0 * W:y1 * W]):016x}"}
+        ok = ok and h["rgba8"] == e["fnv1a64_rgba8"]
+        if prev_host is not None:
+            h["v4"] = f"{rt.frame_hash(prev_host[y0 * W:y1 * W]):016x}"
+            ok = ok and h["v4"] == e["fnv1a64_v4"]
+        got[ty] = h
+    return {"verified": bool(ok), "golden": "tests/golden/c5_rows.json",
+            "rows": {ty: e["rows"] for ty, e in g["tile_rows"].items()}, "hashes": got,
+            "expected": {ty: {"rgba8": e["fnv1a64_rgba8"], "v4": e["fnv1a64_v4"]} for ty, e in g["tile_rows"].items()},
+            "note": "FNV-1a 64 (rt_frame_hash) of the fixture's 32-row tile rows of the last timed frame (the rows "
+                    "0-1, 2160-2161, 4318-4319 among them); the fixture was rendered by the reference's own "
+                    "RenderTile over those tiles and by the oracle (tests/golden/make_c5_rows.py).  The whole "
+                    "frame's ray count has no CPU reference (about 2e11 segments); it is checked equal on every "
+                    "timed step"}
+
+
 def check_frame(rt, args, W, H, S, N, B, cur_host, prev_host, rays):
     """Hashes the last timed frame (RGBA8 and, when given, the v4 running mean)
     with the library's rt_frame_hash and compares it with the committed
     fixture: {"verified": bool or None, "golden": name, ...}."""
     name, g = golden_for(args, W, H, S, N, B)
     if g is None:
+        rg = rows_golden_for(args, W, H, S, N, B)
+        if rg is not None:
+            return check_rows(rt, rg, W, cur_host, prev_host)
         return {"verified": None, "golden": None, "note": "no committed fixture for this workload"}
     got = {"rgba8": f"{rt.frame_hash(cur_host):016x}", "rays": rays}
     ok = got["rgba8"] == g["fnv1a64_rgba8"] and rays == g["rays"]
@@ -230,22 +292,31 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def pmc_record(workload: str, bands: int = 1):
-    """The newest committed rocprofv3 --pmc record of this workload and band
-    split (profiles/rNN_*_pmc.json, written by scripts/pmc_to_json.py; a
-    record without "bands" is a whole-frame, one-GPU one; one marked
-    "superseded_by" was followed by a later kernel's record in the same round)."""
-    for f in sorted((ROOT / "profiles").glob("r*_pmc.json"), reverse=True):
+def pmc_record(workload: str, bands: int = 1, binary_hash: str | None = None):
+    """The committed rocprofv3 --pmc record (profiles/*_pmc.json, written by
+    scripts/pmc_to_json.py) of this workload and band split taken on THIS
+    library's code objects: its `binary_hash` must equal the loaded library's
+    (simd_ray_tracer_amd.code_object_hash, the .hip_fatbin section).  Among
+    several, the one taken last (`taken_unix`).  Returns (record, reason):
+    record None with the reason when no record fits."""
+    best, others = None, 0
+    for f in (ROOT / "profiles").glob("*_pmc.json"):
         try:
             rec = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
-        if rec.get("superseded_by"):  # a later kernel's record of the same round exists
+        if rec.get("workload") != workload or int(rec.get("bands", 1)) != bands:
             continue
-        if rec.get("workload") == workload and int(rec.get("bands", 1)) == bands:
+        if rec.get("binary_hash") != binary_hash:
+            others += 1
+            continue
+        if best is None or (rec.get("taken_unix", 0), f.name) > (best.get("taken_unix", 0), best["file"]):
             rec["file"] = f"profiles/{f.name}"
-            return rec
-    return None
+            best = rec
+    if best is not None:
+        return best, None
+    return None, (f"no committed PMC record of this workload for the loaded code objects (binary_hash "
+                  f"{binary_hash}); {others} record(s) of it belong to other builds")
 
 
 def valu_roofline(pmc, kern_ms: float):
@@ -294,26 +365,35 @@ def valu_roofline(pmc, kern_ms: float):
     return out
 
 
-def workload_name(args, W, H, S, N, B) -> str:
+def workload_name(args, W, H, S, N, B, opts=None) -> str:
+    """The workload a PMC record is matched on: the config and, when a run sets
+    rt_device_options, those options (a record of the brute-force kernel is
+    'C2: ... [Cull=-1, Prefilter=-1]')."""
     preset = all(getattr(args, k) == v for k, v in CONFIGS[args.config].items())
     tag = args.config.upper() if preset else "custom"
     view = "" if args.distance is None else f", camera {args.distance:g} from look-at"
+    o = "" if not opts else " [" + ", ".join(f"{k}={v}" for k, v in sorted(opts.items())) + "]"
     return (f"{tag}: {W}x{H}, {S} spp, {N} spheres, {B} bounces, {'scalar' if args.scalar else 'SIMD'} rules"
-            + ("" if args.scene == 1 else f", {SCENE_NAMES[args.scene]}") + view)
+            + ("" if args.scene == 1 else f", {SCENE_NAMES[args.scene]}") + view + o)
 
 
-def roofline(args, info, kern_ms: float, rays_local: int, rows0: int, W: int, N: int, workload: str, bands: int):
+def roofline(args, info, kern_ms: float, rays_local: int, rows0: int, W: int, N: int, workload: str, bands: int,
+             binary_hash: str | None = None, culled: bool = True):
     """The dominant kernel's roofline object (one device's trace kernel)."""
     ops = rays_local * ops_per_segment(N)
     achieved_alg = ops / (kern_ms / 1e3) / 1e12
     fb_bytes = rows0 * W * (16 + 4)  # accumulation + RGBA8 written once per launch
     hbm_achieved = fb_bytes / (kern_ms / 1e3) / 1e9
-    pmc = pmc_record(workload, bands)
+    pmc, why = pmc_record(workload, bands, binary_hash)
     walks = {0: "any", 1: "groups", 2: "cl1", 3: "cl2", 4: "cl4", 5: "cl1rel", 6: "cl2rel", 7: "cl4rel"}
-    kernel = (f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,CULL,{info['LanesPerPixel']},"
-              f"{'one-wave' if info['OneWaveGroups'] else 'four-wave'},walk={walks.get(info['Walk'], '?')}>")
+    kernel = (f"trace_kernel<{'SIMD' if not args.scalar else 'scalar'},SMEM,{'CULL' if culled else 'NOCULL'},"
+              f"{info['LanesPerPixel']},{'one-wave' if info['OneWaveGroups'] else 'four-wave'},"
+              f"walk={walks.get(info['Walk'], '?')}>")
     roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1), "unit": "TFLOP/s",
-            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": round(kern_ms, 3)}
+            "frac": None, "traffic": None, "kernel": kernel, "kernel_ms": round(kern_ms, 3),
+            "binary_hash": binary_hash}
+    if pmc is None:
+        roof["frac_null_reason"] = why
     if pmc:
         ex = valu_roofline(pmc, kern_ms)
         roof["achieved"], roof["frac"] = ex.pop("achieved"), ex.pop("frac")
@@ -323,6 +403,7 @@ def roofline(args, info, kern_ms: float, rays_local: int, rows0: int, W: int, N:
         roof["traffic"] = round(pmc["hbm_bytes_per_dispatch"]) if "hbm_bytes_per_dispatch" in pmc else None
         roof["executed"] = ex
         roof["source"] = pmc["file"]
+        roof["source_binary_hash"] = pmc["binary_hash"]
         roof["note"] = ("frac = VALU issue occupancy of the trace kernel from the committed PMC record: "
                         "(SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / (1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4); "
                         "frac_lane = frac x lane utilisation (SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)); "
@@ -332,8 +413,10 @@ def roofline(args, info, kern_ms: float, rays_local: int, rows0: int, W: int, N:
                         "traffic = FETCH_SIZE x2 + WRITE_SIZE (KiB), per launch.")
     roof["frac_algorithmic"] = round(achieved_alg / VALU_PEAK_TOPS, 4)
     roof["achieved_algorithmic"] = round(achieved_alg, 2)
-    roof["work_per_launch"] = (f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d brute force; the "
-                               "kernel skips most sphere tests exactly, so this rate can exceed the peak)")
+    roof["work_per_launch"] = (f"{rays_local} segments x (21*{N}+70) f32 ops (SURVEY 8d brute force" +
+                               ("; the kernel skips most sphere tests exactly, so this rate can exceed the peak)"
+                                if culled else "; this kernel tests every sphere for every segment, as "
+                                               "main.cpp:399-430 does)"))
     roof["hbm"] = {"achieved": round(hbm_achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": round(hbm_achieved / HBM_PEAK_GBS, 6), "bytes_per_launch": fb_bytes}
     return roof
@@ -372,6 +455,104 @@ def base_line(args, *, world, elapsed, seg_counted, seg_folded, W, H, S, N, B, w
     }
 
 
+def brute_leg(rt, torch, args, scene, cam, W, H, S, N, B, gpu, stream, binary_hash, workload_of):
+    """SURVEY 8d's roofline on the work it defines: the same frame on a device
+    created with the brute-force kernel (Cull off: no cone cull, no dead-tile
+    fold; Prefilter off: no prefilter, no cluster walk), so every counted
+    segment tests every sphere as main.cpp:399-430 does.  2 warm-up + 3 timed
+    launches (HIP events around each), the last frame checked against the same
+    fixture; frac_algorithmic = segments x (21 N + 70) / kernel time / 78.6 T."""
+    dev = rt.Device(gpu, options=BRUTE)
+    try:
+        dev.upload_scene(scene)
+        dev.reserve(W, H)
+        prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+        cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        ctr = torch.zeros(5, dtype=torch.int64, device="cuda")
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+        for i in range(5):
+            if i >= 2:
+                ev[i - 2][0].record(stream)
+            dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                      rays_ptr=ctr[i].data_ptr(), prev_count=0, frames=S, max_bounce=B, simd=not args.scalar,
+                      band_rows=args.band_rows, accum_zero=True, stream=stream.cuda_stream)
+            if i >= 2:
+                ev[i - 2][1].record(stream)
+        torch.cuda.synchronize()
+        counts = ctr.tolist()
+        ms = sum(a.elapsed_time(b) for a, b in ev) / 3
+        info = dev.last_info()
+        fc = check_frame(rt, args, W, H, S, N, B, cur.cpu().numpy().view("uint32"), prev.cpu().numpy(), counts[-1])
+    finally:
+        dev.close()
+    wl = workload_of(BRUTE)
+    roof = roofline(args, info, ms, counts[-1], H, W, N, wl, 1, binary_hash, culled=False)
+    out = {"ms": round(ms, 3), "frac_algorithmic": roof["frac_algorithmic"],
+           "achieved_algorithmic": roof["achieved_algorithmic"], "frac": roof["frac"],
+           "frac_lane": roof.get("frac_lane"), "achieved": roof["achieved"], "traffic": roof["traffic"],
+           "source": roof.get("source"), "kernel": roof["kernel"], "workload": wl,
+           "segments": counts[-1], "segments_folded": info["SegmentsFolded"],
+           "counted_equal": len(set(counts)) == 1, "verified": fc["verified"], "frame_check": fc,
+           "note": "brute-force kernel of the same frame (rt_device_options Cull=off, Prefilter=off): every "
+                   "counted segment tests every sphere (main.cpp:399-430), so frac_algorithmic = segments x "
+                   "(21N+70) f32 ops / kernel ms / 78.6 T is SURVEY 8d's roofline on work the kernel really "
+                   "executes; frac / frac_lane come from that kernel's committed PMC record (bench.py --brute)"}
+    if "frac_null_reason" in roof:
+        out["frac_null_reason"] = roof["frac_null_reason"]
+    return out
+
+
+def distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, opts):
+    """The headline on samples no launch has seen: timed step i renders frames
+    [S (w+1+i), S (w+2+i)) (PreviousRayCount with RT_FLAG_ACCUM_ZERO: new pixel
+    seeds, main.cpp:797-806's progressive count), so no timed launch repeats
+    the samples its learned wave order and pixel permutation were measured on.
+    The last step is checked bit for bit against a FRESH device's cold render
+    of the same frame range (its first launch: cull pass, split head, no
+    learned order)."""
+    pc0 = S * (args.warmup + 1)
+    prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+    cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    ctr = torch.zeros(args.steps, dtype=torch.int64, device="cuda")
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                  rays_ptr=ctr[i].data_ptr(), prev_count=pc0 + S * i, frames=S, max_bounce=B,
+                  simd=not args.scalar, band_rows=args.band_rows, accum_zero=True, stream=stream.cuda_stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    counts = ctr.tolist()
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    last_pc = pc0 + S * (args.steps - 1)
+    fresh = rt.Device(gpu, options=opts)
+    try:
+        fresh.upload_scene(scene)
+        cprev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+        ccur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        crays = torch.zeros(1, dtype=torch.int64, device="cuda")
+        fresh.trace(cam, width=W, height=H, prev_ptr=cprev.data_ptr(), cur_ptr=ccur.data_ptr(),
+                    rays_ptr=crays.data_ptr(), prev_count=last_pc, frames=S, max_bounce=B, simd=not args.scalar,
+                    band_rows=args.band_rows, accum_zero=True, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        cold_split = fresh.last_info()["SplitHeadFrames"]
+    finally:
+        fresh.close()
+    same = (torch.equal(prev.view(torch.int32), cprev.view(torch.int32)) and torch.equal(cur, ccur)
+            and counts[-1] == int(crays.item()))
+    return {"value": round(sum(counts) / elapsed / 1e6, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "kernel_ms": round(kern_ms, 3), "segments_per_step": counts,
+            "frames": [pc0, last_pc + S], "verified_vs_fresh_device": bool(same),
+            "fresh_device_split_head_frames": cold_split,
+            "note": f"timed step i folds frames [{S}(w+1+i), {S}(w+2+i)) with RT_FLAG_ACCUM_ZERO: every launch "
+                    "traces samples (pixel seeds) no earlier launch traced, with the wave order and pixel "
+                    "permutation learned on other samples; the last step equals a fresh device's cold render of "
+                    "the same frames (v4, RGBA8, ray count)"}
+
+
 def one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, steps: int):
     """The whole frame on one device alone (multi-GPU lines): its RGBA8 frame
     (the --verify reference) and its ms per frame over `steps` warm launches."""
@@ -403,6 +584,8 @@ def main_multi_device(args):
     import __graft_entry__ as graft
 
     rt = graft.load_package()
+    opts = device_options(rt, args)
+    binary_hash = rt.code_object_hash()
     if os.environ.get("BENCH_SHARE_GPU") == "1":
         devices = [0] * args.gpus
     elif args.devices:
@@ -424,7 +607,7 @@ def main_multi_device(args):
     cam = rt.camera_setup(scene, W, H, distance=args.distance)
     transport = rt.RT_MULTI_PEER if args.transport == "peer" else rt.RT_MULTI_RCCL if args.transport == "rccl" \
         else rt.RT_MULTI_AUTO
-    multi = rt.Multi(devices, transport=transport)
+    multi = rt.Multi(devices, transport=transport, options=opts)
     multi.upload_scene(scene)
     # every buffer a call of this geometry needs, allocated now: no call of the
     # timed region allocates or waits for a device (rt_multi_reserve)
@@ -477,12 +660,12 @@ def main_multi_device(args):
     call_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     frame = full.clone()
     # the whole frame on devices[0] alone: the 1-GPU time on this box and the --verify reference
-    dev = rt.Device(d0)
+    dev = rt.Device(d0, options=opts)
     dev.upload_scene(scene)
     ref, one_ms, one_rays = one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, min(args.steps, 5))
     verified = bool(torch.equal(frame, ref)) and one_rays == rays_per_step
     frame_check = check_frame(rt, args, W, H, S, N, B, frame.cpu().numpy().view("uint32"), None, rays_per_step)
-    workload = workload_name(args, W, H, S, N, B)
+    workload = workload_name(args, W, H, S, N, B, opts)
     gather = ("RCCL grouped send/recv to devices[0] (ncclCommInitAll) + rt_assemble scatter, overlapping the next "
               "call's traces" if minfo["Transport"] == rt.RT_MULTI_RCCL else
               "hipMemcpyPeerAsync to devices[0] + rt_assemble scatter, overlapping the next call's traces")
@@ -515,7 +698,9 @@ def main_multi_device(args):
     rows0 = rt.band_local_rows(H, band_rows, args.gpus, slowest)
     share_info = multi.shard_info(slowest)  # what the slowest device's last launch really ran
     line["roofline"] = roofline(args, share_info, per_dev_ms[slowest], rays_per_step // args.gpus, rows0, W, N,
-                                workload, args.gpus)
+                                workload, args.gpus, binary_hash, culled=opts.get("Cull", 0) != -1)
+    if opts:
+        line["config"]["device_options"] = opts
     line["roofline"]["device"] = slowest
     print(json.dumps(line), flush=True)
     dev.close()
@@ -624,6 +809,8 @@ def main():
     import __graft_entry__ as graft
 
     rt = graft.load_package()
+    opts = device_options(rt, args)
+    binary_hash = rt.code_object_hash()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -643,7 +830,7 @@ def main():
     scene = make_scene(rt, args)
     W, H, S, B, N = args.width, args.height, args.spp, args.bounces, args.spheres
     cam = rt.camera_setup(scene, W, H, distance=args.distance)
-    dev = rt.Device(gpu)
+    dev = rt.Device(gpu, options=opts)
     dev.upload_scene(scene)
     band_rows = args.band_rows
     bands = args.sim_ranks if (world == 1 and args.sim_ranks > 1) else world
@@ -825,8 +1012,14 @@ def main():
             comm.close()
         dev.close()
         return
+    legs = {}
+    if world == 1 and bands == 1 and not args.headline_only:
+        legs["distinct"] = distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, opts)
+        if not args.brute and not opts and W * H * S * N <= 2.2 * 1920 * 1080 * 256 * 64:
+            legs["brute"] = brute_leg(rt, torch, args, scene, cam, W, H, S, N, B, gpu, stream, binary_hash,
+                                      lambda o: workload_name(args, W, H, S, N, B, o))
     if rank == 0:
-        workload = workload_name(args, W, H, S, N, B)
+        workload = workload_name(args, W, H, S, N, B, opts)
         line = base_line(args, world=world, elapsed=elapsed, seg_counted=seg_counted, seg_folded=seg_folded,
                          W=W, H=H, S=S, N=N, B=B, workload=workload,
                          parallelism=f"{world} GPU x interleaved {band_rows}-row bands"
@@ -837,7 +1030,15 @@ def main():
                         "note": "first launch for this camera/scene/geometry (cull pass + untrained tile order), "
                                 "wall clock incl. its host synchronisation; the timed steps reuse the cull masks "
                                 "and the learned heaviest-first order"}
-        line["roofline"] = roofline(args, info, kern_ms, rays_local, rows[0], W, N, workload, world)
+        line["roofline"] = roofline(args, info, kern_ms, rays_local, rows[0], W, N, workload, world, binary_hash,
+                                    culled=opts.get("Cull", 0) != -1)
+        if opts:
+            line["config"]["device_options"] = opts
+        if "brute" in legs:
+            line["roofline"]["brute"] = legs["brute"]
+        if "distinct" in legs:
+            line["value_distinct_samples"] = legs["distinct"]["value"]
+            line["distinct_samples"] = legs["distinct"]
         if world > 1:
             line["kernel_ms_max_over_ranks"] = round(kern_ms_max, 3)
         if one_ms is not None and world > 1:
@@ -858,6 +1059,11 @@ def main():
         if line.get("verified") is False:
             print(f"bench.py: the timed frame does NOT match {frame_check.get('golden')}: {frame_check}",
                   file=sys.stderr)
+            raise SystemExit(3)
+        bad = [k for k, leg in (("distinct samples", legs.get("distinct", {}).get("verified_vs_fresh_device")),
+                                ("brute force", legs.get("brute", {}).get("verified"))) if leg is False]
+        if bad:
+            print(f"bench.py: the {' and '.join(bad)} leg's frame does NOT match", file=sys.stderr)
             raise SystemExit(3)
     if comm:
         comm.close()

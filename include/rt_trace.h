@@ -147,9 +147,61 @@ uint64_t rt_pixel_seed(uint32_t x, uint32_t y, uint32_t frame, uint32_t width, u
 
 typedef struct rt_device rt_device;
 
-/* Replaces OnInit's allocation + WorkQueueCreate (main.cpp:658-665). */
+/* Replaces OnInit's allocation + WorkQueueCreate (main.cpp:658-665).  The
+ * device runs the default kernels (every field of rt_device_options 0); the
+ * library reads no environment variable that changes what it computes or
+ * how (only the diagnostic RT_STATS / RT_WAVETIMES hooks, below). */
 int rt_device_create(int hip_device, rt_device **out);
 int rt_device_destroy(rt_device *dev);
+
+/* Kernel and schedule choices of one device, fixed at creation.  Every
+ * choice gives the same bits (each is parity-tested against the oracle); they
+ * exist for A/B measurements and for the brute-force roofline (Cull and
+ * Prefilter RT_OPT_OFF: every counted segment tests every sphere, as
+ * main.cpp:399-430 does).  The reference's only run-time knobs are
+ * render_params (base.h:157-161: ThreadCount, EnableSIMD, SceneIndex), which
+ * rt_trace_desc carries.  Tri-state fields: RT_OPT_DEFAULT (0), RT_OPT_ON (1),
+ * RT_OPT_OFF (-1); numeric fields: 0 = the default.  A zero-filled struct is
+ * rt_device_create's behaviour. */
+#define RT_OPT_DEFAULT 0
+#define RT_OPT_ON 1
+#define RT_OPT_OFF (-1)
+typedef struct rt_device_options {
+    uint32_t Size;               /* sizeof(rt_device_options), or 0                                  */
+    int32_t Cull;                /* primary-ray cone cull and dead-tile fold (default on)            */
+    int32_t Prefilter;           /* secondary-ray prefilter (default: per scene)                     */
+    int32_t PrefilterRelative;   /* per-lane prefilter thresholds (default: per scene)               */
+    int32_t Clusters;            /* cluster walk (default: scenes of <= 64 groups; ON: any size)     */
+    int32_t ClusterCount;        /* k-means top clusters K >= 2 (0: ~1.25 sqrt(n) or n / 8..17)      */
+    int32_t SubClusterSpheres;   /* spheres per sub-cluster of two-level tables (0: 3, per-lane 4)   */
+    int32_t SecondaryThreshold;  /* lanes a secondary round waits for (0: 24/40/48 by walk size)     */
+    int32_t LanesPerPixel;       /* 1/2/4/8/16/32 sample chains per pixel (0: per launch)            */
+    int32_t PixelsPerLane;       /* 1 never, 4 always (0: 4 for one-frame one-lane launches)         */
+    int32_t OneWaveGroups;       /* one wave per workgroup, no LDS image (default on)                */
+    int32_t SphereSourceLds;     /* four-wave kernels read spheres from LDS, not SMEM (default off)  */
+    int32_t SceneInHbm;          /* four-wave kernels keep the scene out of LDS (default off)        */
+    int32_t TablesInLds;         /* four-wave kernels' rsqrt / fold tables in LDS at P <= 8 (on)     */
+    int32_t WalkAny;             /* the one-wave kernel picks its walk at run time (default off)     */
+    int32_t Interleave;          /* wave tiles interleaved over the block tile (default off)         */
+    int32_t MergeRounds;         /* primary + secondary rays in every round (default: <= 2 groups)   */
+    int32_t TileOrder;           /* heaviest-first order learned from earlier launches (default on)  */
+    int32_t WaveOrder;           /* one-wave kernels order waves, not block tiles (default on)       */
+    int32_t PixelSort;           /* a block tile's pixels dealt to its waves by cost (default on)    */
+    int32_t PixelSegment;        /* pixels per dealt unit: 1, 2 or 4 (0: 1)                          */
+    int32_t XcdGroup;            /* a block tile's waves on one XCD (default: launches at P <= 4)    */
+    int32_t SplitFirstLaunch;    /* a key's first long launch measures costs first (default on)      */
+    int32_t HeadSamples;         /* samples per lane of that split's head (0: 8)                     */
+    int32_t SplitParts;          /* launches of the split, 1..8 (0: 2)                               */
+    int32_t SplitGrowth;         /* each leading part this many times the previous (0: 3)            */
+    int32_t OrderLaunches;       /* re-sorts per key before the order is kept (0: 4; -1: none)       */
+    int32_t EncodePass;          /* RGBA8 by a coalesced pass after multi-frame launches (default on) */
+} rt_device_options;
+
+/* rt_device_create with options (NULL: the defaults).  RT_EINVAL for a value
+ * out of range or a Size this library does not know. */
+int rt_device_create_ex(int hip_device, const rt_device_options *options, rt_device **out);
+/* The options the device was created with (as given, defaults left 0). */
+int rt_device_get_options(rt_device *dev, rt_device_options *out);
 
 /* x86 rsqrtss reproduction table (2 x 1024 f32): makes
  * v3::NormalizeFast (x64_math.h:246-257) bit-exact on the GPU. Required. */
@@ -305,6 +357,9 @@ typedef struct rt_multi rt_multi;
 #define RT_MULTI_MAX_DEVICES 16u
 
 int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t transport, rt_multi **out);
+/* rt_multi_create whose devices take `options` (rt_device_create_ex; NULL: the defaults). */
+int rt_multi_create_ex(const int *hip_devices, uint32_t count, uint32_t transport, const rt_device_options *options,
+                       rt_multi **out);
 int rt_multi_destroy(rt_multi *m);
 /* rt_set_rsqrt_table / rt_scene_upload on every device. */
 int rt_multi_set_rsqrt_table(rt_multi *m, const float table[2048]);
@@ -372,6 +427,12 @@ int rt_multi_shard_info(rt_multi *m, uint32_t index, rt_trace_info *out);
  * continuation is RT_EINVAL. */
 #define RT_MULTI_RESERVE_MEAN 1u
 int rt_multi_reserve(rt_multi *m, uint32_t width, uint32_t height, uint32_t band_rows, uint32_t flags);
+
+/* Frames folded into the devices' resident running means, i.e. the
+ * PreviousRayCount a continuation must name; 0 when no mean is resident
+ * (none traced yet, a failed call, a geometry change, or a reservation that
+ * grew the means). */
+int rt_multi_resident_frames(rt_multi *m, uint64_t *out);
 
 /* ----------------------------------- several GPUs, one process per GPU (RCCL) */
 

@@ -209,7 +209,7 @@ void ref_render(const void *spheres, u32 n_spheres, const void *groups, u32 n_gr
 // seeds (patch ii).
 void ref_set_patch(u32 max_bounce, int pixel_seeds) { RtMaxRayBounce = max_bounce; RtPixelSeeds = pixel_seeds; }
 
-struct RtPool { u32 tiles; u32 simd; volatile u32 next; };
+struct RtPool { u32 tiles; u32 simd; volatile u32 next; const u32 *list; };
 static void *rt_worker(void *arg) {
     void **a = (void **)arg;
     RtPool *p = (RtPool *)a[0];
@@ -218,7 +218,7 @@ static void *rt_worker(void *arg) {
         u32 t = __atomic_fetch_add(&p->next, 1u, __ATOMIC_RELAXED);
         if (t >= p->tiles) break;
         work_queue_context Work = {};
-        Work.WorkEntry = t;
+        Work.WorkEntry = p->list ? p->list[t] : t;
         Work.ThreadIndex = index;
         if (p->simd) RenderTile(&Work);
         else RenderTileScalar(&Work);
@@ -230,9 +230,25 @@ static void *rt_worker(void *arg) {
 // one counter, as the reference's work queue deals them (wasm/wasm.cpp:624-694,
 // main.cpp:851-856).  Only meaningful with pixel seeds on (the output is then
 // independent of the schedule); *rays is the sum over the workers.
+void ref_render_tile_list(const void *spheres, u32 n_spheres, const void *groups, u32 n_groups, const void *materials,
+                          u32 n_materials, u32 use_sky, const f32 *cam, u32 width, u32 height, u32 prev_count,
+                          u32 frames, int simd, u32 threads, const u32 *tile_list, u32 n_list, f32 *prev_v4, u32 *cur,
+                          u64 *rays);
+
 void ref_render_threads(const void *spheres, u32 n_spheres, const void *groups, u32 n_groups, const void *materials,
                         u32 n_materials, u32 use_sky, const f32 *cam, u32 width, u32 height, u32 prev_count,
                         u32 frames, int simd, u32 threads, f32 *prev_v4, u32 *cur, u64 *rays) {
+    ref_render_tile_list(spheres, n_spheres, groups, n_groups, materials, n_materials, use_sky, cam, width, height,
+                         prev_count, frames, simd, threads, 0, 0, prev_v4, cur, rays);
+}
+
+// ref_render_threads over a subset of the 32x32 tiles (work entries tile_list[0..n_list), row-major
+// tile indices as main.cpp:362-368 decodes them), e.g. whole tile rows of a frame too large to render
+// entirely (C5).  tile_list NULL: every tile.
+void ref_render_tile_list(const void *spheres, u32 n_spheres, const void *groups, u32 n_groups, const void *materials,
+                          u32 n_materials, u32 use_sky, const f32 *cam, u32 width, u32 height, u32 prev_count,
+                          u32 frames, int simd, u32 threads, const u32 *tile_list, u32 n_list, f32 *prev_v4, u32 *cur,
+                          u64 *rays) {
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
     static thread_context Context[64];
@@ -251,7 +267,8 @@ void ref_render_threads(const void *spheres, u32 n_spheres, const void *groups, 
     for (u32 i = 0; i < threads; ++i) { Context[i].RandomState.Seed = 0; Context[i].RaysCastInThread = 0; }
     ThreadContexts = Context;
     RtPool pool;
-    pool.tiles = CameraInfo.TilesX * ((height + TileSize - 1) / TileSize);
+    pool.tiles = tile_list ? n_list : CameraInfo.TilesX * ((height + TileSize - 1) / TileSize);
+    pool.list = tile_list;
     pool.simd = simd ? 1u : 0u;
     pthread_t th[64];
     void *args[64][2];

@@ -1,23 +1,27 @@
 # Same-box A/B of variants (the one A/B launcher; gpurun -- 'bash scripts/gpu_ab.sh').
-#   VARIANTS  ';'-separated; each is a list of env assignments, e.g.
-#             "RT_X=0;RT_SEC_THRESHOLD=24;RT_TRACE_LIB=librt_trace_base.so" (library builds:
-#             scripts/build_base_lib.sh, or make -C simd-ray-tracer_amd variant NAME=.. KFLAGS=..)
+#   VARIANTS  ';'-separated; each a list of tokens (scripts/variant.sh): rt_device_options as bench
+#             arguments and library builds as env, e.g. "default;--opt SecondaryThreshold=16;
+#             RT_TRACE_LIB=librt_trace_base.so" (library builds: scripts/build_base_lib.sh, or
+#             make -C simd-ray-tracer_amd variant NAME=.. KFLAGS=..)
 #   CONFIGS   ';'-separated bench.py argument sets, "c2" = the defaults
 #             (default: "c2;--sim-ranks 8 --sim-index 3", the 8-rank share)
 #   ROUNDS    interleaved repetitions (default 3)
-#   PARITY=1  run the GPU suite under each variant first (stops at the first failure)
+#   PARITY=1  run the GPU suite under each library build first (stops at the first failure; options
+#             are parity-tested by tests/test_gpu_parity.py's VARIANT_OPTIONS)
 #   STEPS / WARMUP  bench steps (default 10 / 6)
 # Prints one line per run: round, variant, config, Mrays/s, ms per step, kernel ms, cold ms.
 set -o pipefail
 mkdir -p gpurun_out
-IFS=';' read -ra VAR <<< "${VARIANTS:-RT_X=0}"
+. "$(dirname "$0")/variant.sh"
+IFS=';' read -ra VAR <<< "${VARIANTS:-default}"
 IFS=';' read -ra CFG <<< "${CONFIGS:-c2;--sim-ranks 8 --sim-index 3}"
 ROUNDS=${ROUNDS:-3}
 if [ "${PARITY:-0}" = 1 ]; then
   i=0
   for v in "${VAR[@]}"; do
     i=$((i+1))
-    env $v timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 200 \
+    split_variant "$v"
+    env "${VENV[@]}" RT_X=0 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 200 \
       --timeout-method thread > gpurun_out/ab_pytest_$i.log 2>&1
     rc=$?; echo "parity [$v] rc=$rc $(tail -1 gpurun_out/ab_pytest_$i.log)"
     [ $rc -ne 0 ] && { tail -30 gpurun_out/ab_pytest_$i.log; exit $rc; }
@@ -27,7 +31,9 @@ for r in $(seq $ROUNDS); do
   for v in "${VAR[@]}"; do
     for c in "${CFG[@]}"; do
       args=$c; [ "$c" = "c2" ] && args=""
-      env $v timeout -k 10 180 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-6} --no-cpu-baseline $args \
+      split_variant "$v"
+      env "${VENV[@]}" RT_X=0 timeout -k 10 180 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-6} --no-cpu-baseline \
+        --headline-only "${VARGS[@]}" $args \
         > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
       python - "$r" "$v" "$c" <<'PY'
 import json, sys

@@ -4,10 +4,10 @@ set -o pipefail
 tag=${1:-fc}
 out=gpurun_out/${tag}_forecast.txt
 : > $out
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline 2>/dev/null \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only 2>/dev/null \
   | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'c2_before': d['value'], 'ms_per_step': d['ms_per_step']}))" >> $out || exit 1
 for g in 8 4 2; do bash scripts/gpu_simranks_all.sh $g >> $out 2>&1 || exit 1; done
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline 2>/dev/null \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only 2>/dev/null \
   | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'c2_after': d['value'], 'ms_per_step': d['ms_per_step']}))" >> $out || exit 1
 python - $out <<'PY'
 import json, sys

@@ -15,6 +15,6 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_IFETCH GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set -d gpurun_out/pmc_${tag}_$i -o p --output-format csv -- python bench.py --steps 1 --warmup ${PMC_WARMUP:-7} --no-cpu-baseline "$@" > gpurun_out/pmc_${tag}_$i.log 2>&1 || { tail -5 gpurun_out/pmc_${tag}_$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $set -d gpurun_out/pmc_${tag}_$i -o p --output-format csv -- python bench.py --steps 1 --warmup ${PMC_WARMUP:-7} --no-cpu-baseline --headline-only "$@" > gpurun_out/pmc_${tag}_$i.log 2>&1 || { tail -5 gpurun_out/pmc_${tag}_$i.log; exit 1; }
 done
 echo "pmc passes done: $i"

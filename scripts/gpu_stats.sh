@@ -1,15 +1,17 @@
 # Scheduling counters of the -DRTK_STATS build (make -C simd-ray-tracer_amd variant NAME=stats KFLAGS=-DRTK_STATS)
-# for each ';'-separated env variant in $VARIANTS and each bench config in $CONFIGS (';'-separated, "c2" = defaults).
+# for each ';'-separated variant in $VARIANTS (scripts/variant.sh) and each bench config in $CONFIGS (';'-separated, "c2" = defaults).
 # Prints the lane-trip shares: done (finished lanes), primary/secondary lanes per round.
 set -o pipefail
 mkdir -p gpurun_out
-IFS=';' read -ra VAR <<< "${VARIANTS:-RT_X=0}"
+. "$(dirname "$0")/variant.sh"
+IFS=';' read -ra VAR <<< "${VARIANTS:-default}"
 IFS=';' read -ra CFG <<< "${CONFIGS:-c2}"
 for v in "${VAR[@]}"; do
   for c in "${CFG[@]}"; do
     args=$c; [ "$c" = "c2" ] && args=""
-    env RT_STATS=1 RT_TRACE_LIB=librt_trace_stats.so $v timeout -k 10 180 python bench.py --steps 1 --warmup ${WARMUP:-6} \
-      --no-cpu-baseline $args > gpurun_out/st.json 2> gpurun_out/st.err || { tail -5 gpurun_out/st.err; exit 1; }
+    split_variant "$v"
+    env RT_STATS=1 RT_TRACE_LIB=librt_trace_stats.so "${VENV[@]}" timeout -k 10 180 python bench.py --steps 1 \
+      --warmup ${WARMUP:-6} --no-cpu-baseline --headline-only "${VARGS[@]}" $args > gpurun_out/st.json 2> gpurun_out/st.err || { tail -5 gpurun_out/st.err; exit 1; }
     python - "$v" "$c" <<'PY'
 import json, sys
 d = json.loads([l for l in open("gpurun_out/st.json") if l.startswith("{")][-1])

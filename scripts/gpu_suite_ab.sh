@@ -5,5 +5,5 @@ tag=${1:-ab}
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread \
   > gpurun_out/${tag}_pytest.log 2>&1; rc=$?; tail -1 gpurun_out/${tag}_pytest.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/${tag}_pytest.log | head; exit $rc; }
-VARIANTS="RT_TRACE_LIB=librt_trace_base.so;RT_X=0" CONFIGS="${CONFIGS:-c2;--config rtw;--sim-ranks 8 --sim-index 0}" \
+VARIANTS="RT_TRACE_LIB=librt_trace_base.so;default" CONFIGS="${CONFIGS:-c2;--config rtw;--sim-ranks 8 --sim-index 0}" \
   ROUNDS=${ROUNDS:-3} bash scripts/gpu_ab.sh

@@ -1,10 +1,11 @@
 # HBM write/fetch bytes of the trace kernel's last (warm) dispatch per env variant and config:
 # one FETCH_SIZE and one WRITE_SIZE pass each (kernel-trace counters only).
-#   VARIANTS ';'-separated env assignments; CONFIGS ';'-separated bench args ("c2" = defaults); WARMUP (default 8)
+#   VARIANTS ';'-separated variants (scripts/variant.sh); CONFIGS ';'-separated bench args ("c2" = defaults); WARMUP (default 8)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-IFS=';' read -ra VAR <<< "${VARIANTS:-RT_X=0}"
+. scripts/variant.sh
+IFS=';' read -ra VAR <<< "${VARIANTS:-default}"
 IFS=';' read -ra CFG <<< "${CONFIGS:-c2}"
 n=0
 for v in "${VAR[@]}"; do
@@ -12,8 +13,9 @@ for v in "${VAR[@]}"; do
     args=$c; [ "$c" = "c2" ] && args=""
     for ctr in FETCH_SIZE WRITE_SIZE; do
       n=$((n+1))
-      env $v timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/wr_$n -o p --output-format csv -- python bench.py --steps 1 \
-        --warmup ${WARMUP:-8} --no-cpu-baseline $args > gpurun_out/wr_$n.log 2>&1 || { tail -5 gpurun_out/wr_$n.log; exit 1; }
+      split_variant "$v"
+      env "${VENV[@]}" RT_X=0 timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/wr_$n -o p --output-format csv -- \
+        python bench.py --steps 1 --warmup ${WARMUP:-8} --no-cpu-baseline --headline-only "${VARGS[@]}" $args > gpurun_out/wr_$n.log 2>&1 || { tail -5 gpurun_out/wr_$n.log; exit 1; }
       python - "$v" "$c" "$ctr" gpurun_out/wr_$n <<'PY'
 import csv, glob, sys
 rows = [r for f in glob.glob(sys.argv[4] + "/**/*counter_collection.csv", recursive=True) for r in csv.DictReader(open(f))

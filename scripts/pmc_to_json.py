@@ -3,7 +3,10 @@ record for the trace kernel that bench.py reports as roofline.traffic and as
 the executed-work roofline fraction.
 
 usage: python scripts/pmc_to_json.py gpurun_out pmc_r02_c2_ profiles/r02_c2_pmc.json "<workload>" [bands]
-(bands: the band split of a --sim-ranks share, e.g. 8; bench.py matches records on workload + bands)
+(bands: the band split of a --sim-ranks share, e.g. 8; bench.py matches records on workload + bands +
+binary_hash).  Run it on the GPU box right after the passes: the record is stamped with the code-object
+hash of the library the passes ran (simd_ray_tracer_amd.code_object_hash, or RT_TRACE_LIB's build) and the
+time it was folded (taken_unix); bench.py uses a record only for a library with the same hash.
 
 Per pass only the LAST trace_kernel dispatch is kept (the bench's timed, warm
 launch; the earlier ones are the cold launch and warm-up launches that learn
@@ -22,7 +25,13 @@ import collections
 import csv
 import glob
 import json
+import os
+import pathlib
 import sys
+import time
+
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+import __graft_entry__ as graft  # noqa: E402  (the package's code_object_hash: reads the .so, no GPU)
 
 root, prefix, out, workload = sys.argv[1:5]
 bands = int(sys.argv[5]) if len(sys.argv) > 5 else 1
@@ -46,8 +55,11 @@ for f in sorted(glob.glob(f"{root}/{prefix}*/**/*counter_collection.csv", recurs
 g = per.pop("GRBM_GUI_ACTIVE_passes", [])
 if g:
     per["GRBM_GUI_ACTIVE"] = sum(g) / len(g)
+rt = graft.load_package()
+lib = rt.LIB_PATH
 rec = {"workload": workload, "bands": bands, "kernel": kernel, "dispatch": "last trace_kernel dispatch of each pass (warm)",
-       "counters_per_dispatch": per}
+       "counters_per_dispatch": per, "binary_hash": rt.code_object_hash(lib), "library": lib.name,
+       "taken_unix": int(time.time()), "passes": len(glob.glob(f"{root}/{prefix}*/"))}
 if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     rec["hbm_bytes_per_dispatch"] = 2.0 * per["FETCH_SIZE"] * 1024 + per["WRITE_SIZE"] * 1024
 if "GRBM_GUI_ACTIVE" in per:

@@ -2,7 +2,7 @@
 env: SPP (256), SIM_RANKS (1: whole frame; G: rank 0's bands of a G-GPU split),
 SCENE (1) / SPHERES (64) / BOUNCES (8), CONTINUE (1: launches continue the running mean,
 as OnRender's frames do; default: every launch restarts it),
-RT_LANES_PER_PIXEL (auto), LAUNCHES (8: the learned order settles), SAVE (a .npz
+LPP (lanes per pixel, rt_device_options LanesPerPixel; 0 auto), LAUNCHES (8: the learned order settles), SAVE (a .npz
 path: the raw per-wave {start, end} of the last launch, indexed 4 * block tile + wave,
 for offline schedule simulation: scripts/sched_sim.py)."""
 import os
@@ -21,7 +21,7 @@ if N < scene.ScalarSpheres.Count:
     scene = rt.scene_prefix(scene, N)
 cont = os.environ.get("CONTINUE") == "1"
 cam = rt.camera_setup(scene, W, H)
-dev = rt.Device(0)
+dev = rt.Device(0, options={"LanesPerPixel": int(os.environ.get("LPP", "0"))})
 dev.upload_scene(scene)
 G = int(os.environ.get("SIM_RANKS", "1"))
 rows = rt.band_local_rows(H, 8, G, 0)

@@ -94,6 +94,44 @@ class RtTraceInfo(ctypes.Structure):  # rt_trace_last_info
         "GroupsPerRuleSet", "SplitHeadFrames", "OneWaveGroups", "Walk", "PixelsPerLane", "PixelsSorted", "BufferGrowths")]
 
 
+OPTION_FIELDS = ("Cull", "Prefilter", "PrefilterRelative", "Clusters", "ClusterCount", "SubClusterSpheres",
+                 "SecondaryThreshold", "LanesPerPixel", "PixelsPerLane", "OneWaveGroups", "SphereSourceLds",
+                 "SceneInHbm", "TablesInLds", "WalkAny", "Interleave", "MergeRounds", "TileOrder", "WaveOrder",
+                 "PixelSort", "PixelSegment", "XcdGroup", "SplitFirstLaunch", "HeadSamples", "SplitParts",
+                 "SplitGrowth", "OrderLaunches", "EncodePass")
+RT_OPT_DEFAULT, RT_OPT_ON, RT_OPT_OFF = 0, 1, -1
+
+
+class RtDeviceOptions(ctypes.Structure):  # rt_device_options: kernel / schedule choices, 0 = default
+    _fields_ = [("Size", c_uint32)] + [(n, ctypes.c_int32) for n in OPTION_FIELDS]
+
+
+def device_options(options: Optional[dict]) -> Optional[RtDeviceOptions]:
+    """rt_device_options from {"Cull": RT_OPT_OFF, "LanesPerPixel": 16, ...} (None: the defaults).
+    Switches also take True / False for RT_OPT_ON / RT_OPT_OFF."""
+    if not options:
+        return None
+    o = RtDeviceOptions()
+    o.Size = ctypes.sizeof(RtDeviceOptions)
+    for k, v in options.items():
+        if k not in OPTION_FIELDS:
+            raise KeyError(f"unknown device option {k!r} (rt_device_options: {', '.join(OPTION_FIELDS)})")
+        setattr(o, k, (RT_OPT_ON if v else RT_OPT_OFF) if isinstance(v, bool) else int(v))
+    return o
+
+
+def parse_options(items) -> dict:
+    """["Cull=off", "LanesPerPixel=16", ...] (bench.py --opt) -> an options dict."""
+    out = {}
+    for it in items or ():
+        k, _, v = it.partition("=")
+        v = v.strip().lower()
+        out[k.strip()] = {"on": RT_OPT_ON, "off": RT_OPT_OFF, "default": RT_OPT_DEFAULT}.get(v, None)
+        if out[k.strip()] is None:
+            out[k.strip()] = int(v)
+    return out
+
+
 class RtMultiInfo(ctypes.Structure):  # rt_multi_get_info
     _fields_ = [(n, c_uint32) for n in ("DeviceCount", "Transport", "BandRows", "MaxLocalRows")] + [
         ("SegmentsFolded", c_uint64)]
@@ -121,6 +159,8 @@ SIGNATURES = {
                                 POINTER(RtCameraInfo)]),
     "rt_pixel_seed": (c_uint64, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint32]),
     "rt_device_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "rt_device_create_ex": (c_int, [c_int, POINTER(RtDeviceOptions), POINTER(c_void_p)]),
+    "rt_device_get_options": (c_int, [c_void_p, POINTER(RtDeviceOptions)]),
     "rt_device_destroy": (c_int, [c_void_p]),
     "rt_set_rsqrt_table": (c_int, [c_void_p, c_void_p]),
     "rt_rsqrt_table_builtin": (c_int, [c_void_p]),
@@ -134,6 +174,8 @@ SIGNATURES = {
     "rt_encode_rgba8": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "rt_device_synchronize": (c_int, [c_void_p]),
     "rt_multi_create": (c_int, [POINTER(c_int), c_uint32, c_uint32, POINTER(c_void_p)]),
+    "rt_multi_create_ex": (c_int, [POINTER(c_int), c_uint32, c_uint32, POINTER(RtDeviceOptions), POINTER(c_void_p)]),
+    "rt_multi_resident_frames": (c_int, [c_void_p, POINTER(c_uint64)]),
     "rt_multi_destroy": (c_int, [c_void_p]),
     "rt_multi_set_rsqrt_table": (c_int, [c_void_p, c_void_p]),
     "rt_multi_scene_upload": (c_int, [c_void_p, POINTER(RtScene)]),
@@ -336,9 +378,11 @@ def rsqrt_table_builtin() -> np.ndarray:
 class Device:
     """One GPU: rsqrt table, uploaded scene, trace launches (rt_device)."""
 
-    def __init__(self, ordinal: int = 0, rsqrt_table: Optional[np.ndarray] = None):
+    def __init__(self, ordinal: int = 0, rsqrt_table: Optional[np.ndarray] = None, options: Optional[dict] = None):
         h = c_void_p()
-        _check(lib().rt_device_create(ordinal, ctypes.byref(h)), "rt_device_create")
+        o = device_options(options)
+        _check(lib().rt_device_create_ex(ordinal, ctypes.byref(o) if o is not None else None, ctypes.byref(h)),
+               "rt_device_create")
         self.handle = h
         table = rsqrt_table_builtin() if rsqrt_table is None else np.ascontiguousarray(rsqrt_table, np.float32)
         _check(lib().rt_set_rsqrt_table(self.handle, table.ctypes.data), "rt_set_rsqrt_table")
@@ -347,6 +391,12 @@ class Device:
     def upload_scene(self, scene: RtScene) -> None:
         _check(lib().rt_scene_upload(self.handle, ctypes.byref(scene)), "rt_scene_upload")
         self._scene = scene
+
+    def options(self) -> dict:
+        """The non-default rt_device_options the device was created with."""
+        o = RtDeviceOptions()
+        _check(lib().rt_device_get_options(self.handle, ctypes.byref(o)), "rt_device_get_options")
+        return {n: int(getattr(o, n)) for n in OPTION_FIELDS if getattr(o, n)}
 
     def trace(self, cam: RtCameraInfo, *, width: int, height: int, prev_ptr: int, cur_ptr: int, rays_ptr: int,
               prev_count: int = 0, frames: int = 1, max_bounce: int = 5, simd: bool = True,
@@ -424,10 +474,13 @@ class Multi:
     """Several GPUs from one process (rt_multi): interleaved row bands, one
     device each, gathered to devices[0] over RCCL or peer copies."""
 
-    def __init__(self, devices, transport: int = RT_MULTI_AUTO, rsqrt_table: Optional[np.ndarray] = None):
+    def __init__(self, devices, transport: int = RT_MULTI_AUTO, rsqrt_table: Optional[np.ndarray] = None,
+                 options: Optional[dict] = None):
         devs = (c_int * len(devices))(*devices)
         h = c_void_p()
-        _check(lib().rt_multi_create(devs, len(devices), transport, ctypes.byref(h)), "rt_multi_create")
+        o = device_options(options)
+        _check(lib().rt_multi_create_ex(devs, len(devices), transport, ctypes.byref(o) if o is not None else None,
+                                        ctypes.byref(h)), "rt_multi_create")
         self.handle = h
         table = rsqrt_table_builtin() if rsqrt_table is None else np.ascontiguousarray(rsqrt_table, np.float32)
         _check(lib().rt_multi_set_rsqrt_table(self.handle, table.ctypes.data), "rt_multi_set_rsqrt_table")
@@ -470,6 +523,12 @@ class Multi:
         """rt_multi_reserve: pre-size every buffer a call of this geometry needs."""
         _check(lib().rt_multi_reserve(self.handle, width, height, band_rows, RT_MULTI_RESERVE_MEAN if mean else 0),
                "rt_multi_reserve")
+
+    def resident_frames(self) -> int:
+        """Frames folded into the devices' resident means (0: none resident, rt_multi_resident_frames)."""
+        n = c_uint64(0)
+        _check(lib().rt_multi_resident_frames(self.handle, ctypes.byref(n)), "rt_multi_resident_frames")
+        return int(n.value)
 
     def info(self) -> dict:
         i = RtMultiInfo()
@@ -612,6 +671,29 @@ def write_image(image: np.ndarray, path, flip_y: bool = True) -> None:
     fn = lib().rt_image_write_png if path.lower().endswith(".png") else lib().rt_image_write_ppm
     name = "rt_image_write_png" if path.lower().endswith(".png") else "rt_image_write_ppm"
     _check(fn(ctypes.byref(img), path.encode(), RT_IMAGE_FLIP_Y if flip_y else 0), name)
+
+
+def code_object_hash(path=None) -> str:
+    """SHA-256 (first 16 hex digits) of the gfx950 code objects a library
+    carries: the bytes of its ELF `.hip_fatbin` section (every kernel
+    translation unit's offload bundle).  Host-only changes leave it alone; any
+    kernel change moves it.  bench.py uses a committed PMC record only when
+    the record's `binary_hash` equals the loaded library's.  Reads the file
+    (no GPU, no load)."""
+    import hashlib
+    import struct
+    data = pathlib.Path(path or LIB_PATH).read_bytes()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        raise RtError(f"{path or LIB_PATH}: not an ELF64 file")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stroff = secs[shstrndx][4]
+    for name, _, _, _, off, size in secs:
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise RtError(f"{path or LIB_PATH}: no .hip_fatbin section")
 
 
 def frame_hash(a) -> int:

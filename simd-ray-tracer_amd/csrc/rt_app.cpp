@@ -168,8 +168,11 @@ int reserve_launch(uint32_t w, uint32_t h) {
     if (g_app.multi) {
         rc = rt_multi_reserve(g_app.multi, w, h, 8u, 0u);
         // a reservation that grows the devices' resident means drops them (rt_multi_reserve):
-        // restart the mean at the next call (a resize restarts it anyway)
-        if (g_app.width && g_app.prev_count) g_app.restart_pending = true;
+        // once any frame has been traced (the mean holds frame 0 even at prev_count 0), the next
+        // call must restart it rather than continue (a resize restarts it anyway)
+        uint64_t held = 0;
+        if (g_app.width && (rt_multi_resident_frames(g_app.multi, &held) != RT_OK || held == 0))
+            g_app.restart_pending = true;
     } else {
         rc = rt_device_reserve(g_app.dev, w, h);
     }
@@ -254,8 +257,12 @@ extern "C" int rt_on_init_devices(rt_init_params *params, const int *hip_devices
     (void)hipMemset(g_app.d_rays, 0, sizeof(uint64_t));
     g_app.ready = true;
     // the window OnInit asks the platform for (main.cpp:649-650): frames up to
-    // that size need no allocation in the frame loop
-    return rt_on_render_reserve(1280u, 720u);
+    // that size need no allocation in the frame loop.  Best effort: a failed
+    // reservation (no memory) leaves the frames to grow on the first resize, as
+    // they would without one, so the initialised driver stays usable.
+    (void)rt_on_render_reserve(1280u, 720u);
+    (void)hipGetLastError();
+    return RT_OK;
 }
 
 extern "C" int rt_on_render_reserve(uint32_t width, uint32_t height) {

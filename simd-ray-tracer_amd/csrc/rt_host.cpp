@@ -131,6 +131,8 @@ struct rt_device {
     size_t wave_times_cap = 0;
     bool want_wave_times = false;
     rt_trace_info last{};  // what the last rt_trace launched (rt_trace_last_info)
+    rt_device_options opt{};  // as created (rt_device_get_options)
+    uint32_t cluster_k = 0, sub_spheres = 0;  // cluster_table's K and sub-cluster size (0: per scene)
 };
 
 static thread_local char g_err[512];
@@ -165,9 +167,76 @@ int rt_fail(int code, const char *fmt, ...) {
 
 extern "C" const char *rt_last_error(void) { return g_err; }
 
-extern "C" int rt_device_create(int hip_device, rt_device **out) {
+extern "C" int rt_device_create(int hip_device, rt_device **out) { return rt_device_create_ex(hip_device, nullptr, out); }
+
+// rt_device_options -> the device's switches (rt_trace.h: 0 = the default, RT_OPT_ON / RT_OPT_OFF)
+static int apply_options(rt_device *d, const rt_device_options *o) {
+    if (!o) return RT_OK;
+    if (o->Size != 0 && o->Size != sizeof(rt_device_options))
+        return fail(RT_EINVAL, "rt_device_options: Size %u, this library's is %zu", o->Size, sizeof(rt_device_options));
+    const int32_t tri[] = {o->Cull, o->Prefilter, o->PrefilterRelative, o->Clusters, o->OneWaveGroups,
+                           o->SphereSourceLds, o->SceneInHbm, o->TablesInLds, o->WalkAny, o->Interleave,
+                           o->MergeRounds, o->TileOrder, o->WaveOrder, o->PixelSort, o->XcdGroup,
+                           o->SplitFirstLaunch, o->EncodePass};
+    for (const int32_t v : tri)
+        if (v < -1 || v > 1) return fail(RT_EINVAL, "rt_device_options: a switch is %d (RT_OPT_DEFAULT/ON/OFF)", v);
+    const int32_t lpp = o->LanesPerPixel;
+    if (!(lpp == 0 || lpp == 1 || lpp == 2 || lpp == 4 || lpp == 8 || lpp == 16 || lpp == 32))
+        return fail(RT_EINVAL, "rt_device_options: LanesPerPixel %d", lpp);
+    if (!(o->PixelsPerLane == 0 || o->PixelsPerLane == 1 || o->PixelsPerLane == 4))
+        return fail(RT_EINVAL, "rt_device_options: PixelsPerLane %d", o->PixelsPerLane);
+    if (!(o->PixelSegment == 0 || o->PixelSegment == 1 || o->PixelSegment == 2 || o->PixelSegment == 4))
+        return fail(RT_EINVAL, "rt_device_options: PixelSegment %d", o->PixelSegment);
+    if (o->SplitParts < 0 || o->SplitParts > 8 || o->HeadSamples < 0 || o->SplitGrowth < 0 || o->OrderLaunches < -1 ||
+        o->SecondaryThreshold < 0 || o->SecondaryThreshold > 64 || o->ClusterCount < 0 || o->ClusterCount == 1 ||
+        o->SubClusterSpheres < 0)
+        return fail(RT_EINVAL, "rt_device_options: a count is out of range");
+    auto on = [](int32_t v, bool dflt) { return v == RT_OPT_DEFAULT ? dflt : v == RT_OPT_ON; };
+    d->opt = *o;
+    d->opt.Size = sizeof(rt_device_options);
+    d->cull = on(o->Cull, true) ? 1 : 0;
+    d->prefilter_env = o->Prefilter == RT_OPT_DEFAULT ? -1 : o->Prefilter == RT_OPT_ON ? 1 : 0;
+    d->pf_rel_env = o->PrefilterRelative == RT_OPT_DEFAULT ? -1 : o->PrefilterRelative == RT_OPT_ON ? 1 : 0;
+    d->clusters_env = o->Clusters == RT_OPT_DEFAULT ? 1 : o->Clusters == RT_OPT_ON ? 2 : 0;
+    d->cluster_k = (uint32_t)o->ClusterCount;
+    d->sub_spheres = (uint32_t)o->SubClusterSpheres;
+    d->sec_threshold = (uint32_t)o->SecondaryThreshold;
+    d->lanes_per_pixel = lpp;
+    d->pixels_per_lane_env = o->PixelsPerLane;
+    d->solo_env = on(o->OneWaveGroups, true) ? 1 : 0;
+    d->src = on(o->SphereSourceLds, false) ? kSrcLds : kSrcSmem;
+    d->scene_global_env = on(o->SceneInHbm, false) ? 1 : 0;
+    d->tables_global_env = on(o->TablesInLds, true) ? 0 : 1;
+    d->walk_any_env = on(o->WalkAny, false) ? 1 : 0;
+    d->interleave_env = on(o->Interleave, false) ? 1 : 0;
+    d->merge_env = o->MergeRounds == RT_OPT_DEFAULT ? -1 : o->MergeRounds == RT_OPT_ON ? 1 : 0;
+    d->tile_sched = on(o->TileOrder, true) ? 1 : 0;
+    d->wave_order_env = on(o->WaveOrder, true) ? 1 : 0;
+    d->pixel_sort_env = on(o->PixelSort, true) ? 1 : 0;
+    if (o->PixelSegment) d->pixel_seg = (uint32_t)o->PixelSegment;
+    d->xcd_group_env = o->XcdGroup == RT_OPT_DEFAULT ? -1 : o->XcdGroup == RT_OPT_ON ? 1 : 0;
+    d->split_env = on(o->SplitFirstLaunch, true) ? 1 : 0;
+    if (o->HeadSamples) d->head_samples = (uint32_t)o->HeadSamples;
+    if (o->SplitParts) d->split_parts = (uint32_t)o->SplitParts;
+    if (o->SplitGrowth) d->split_growth = (uint32_t)o->SplitGrowth;
+    if (o->OrderLaunches) d->order_launches = o->OrderLaunches < 0 ? 0u : (uint32_t)o->OrderLaunches;
+    d->cur_pass = on(o->EncodePass, true) ? 1u : 0u;
+    return RT_OK;
+}
+
+extern "C" int rt_device_get_options(rt_device *d, rt_device_options *out) {
+    if (!d || !out) return fail(RT_EINVAL, "rt_device_get_options: NULL argument");
+    *out = d->opt;
+    return RT_OK;
+}
+
+extern "C" int rt_device_create_ex(int hip_device, const rt_device_options *options, rt_device **out) {
     DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!out) return fail(RT_EINVAL, "rt_device_create: out is NULL");
+    {  // options are checked before anything touches a device (a host-only rt_device)
+        rt_device probe;
+        if (const int rc = apply_options(&probe, options)) return rc;
+    }
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
         return fail(RT_ENODEV, "rt_device_create: no HIP device visible");
@@ -201,61 +270,14 @@ extern "C" int rt_device_create(int hip_device, rt_device **out) {
         if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
             d->cu_count = (uint32_t)prop.multiProcessorCount;
     }
-    const char *src = getenv("RT_SPHERE_SRC");
-    if (src && strcmp(src, "lds") == 0) d->src = kSrcLds;
-    const char *cull = getenv("RT_CULL");  // 0: brute-force primary rays too (A/B)
-    if (cull && cull[0] == '0') d->cull = 0;
-    const char *thr = getenv("RT_SEC_THRESHOLD");
-    if (thr) d->sec_threshold = (uint32_t)atoi(thr);
-    const char *pf = getenv("RT_PREFILTER");  // secondary-ray prefilter: 0 off, 1 on, unset = per-scene auto
-    if (pf && (pf[0] == '0' || pf[0] == '1')) d->prefilter_env = pf[0] - '0';
-    const char *pr = getenv("RT_PF_REL");
-    if (pr && (pr[0] == '0' || pr[0] == '1')) d->pf_rel_env = pr[0] - '0';
-    const char *to = getenv("RT_TILE_ORDER");
-    if (to && to[0] == '0') d->tile_sched = 0;
-    const char *clu = getenv("RT_CLUSTERS");
-    if (clu && (clu[0] == '0' || clu[0] == '2')) d->clusters_env = clu[0] - '0';
-    const char *pe = getenv("RT_PROBE");
-    if (pe && pe[0] == '0') d->split_env = 0;
-    const char *hs = getenv("RT_HEAD_SAMPLES");
-    if (hs && atoi(hs) > 0) d->head_samples = (uint32_t)atoi(hs);
-    const char *sp = getenv("RT_SPLIT_PARTS");
-    if (sp && atoi(sp) >= 1 && atoi(sp) <= 8) d->split_parts = (uint32_t)atoi(sp);
-    const char *sgr = getenv("RT_SPLIT_GROWTH");
-    if (sgr && atoi(sgr) >= 1) d->split_growth = (uint32_t)atoi(sgr);
-    const char *ol = getenv("RT_ORDER_LAUNCHES");
-    if (ol) d->order_launches = (uint32_t)atoi(ol);
-    const char *il = getenv("RT_INTERLEAVE");
-    if (il && (il[0] == '0' || il[0] == '1')) d->interleave_env = il[0] - '0';
-    const char *sg = getenv("RT_SCENE_GLOBAL");
-    if (sg && sg[0] == '1') d->scene_global_env = 1;
-    const char *tl = getenv("RT_TABLES_LDS");  // 0: rsqrt + fold tables read through the caches at every size (A/B)
-    if (tl && tl[0] == '0') d->tables_global_env = 1;
-    const char *wo = getenv("RT_WAVE_ORDER");
-    if (wo && wo[0] == '0') d->wave_order_env = 0;
-    const char *wa = getenv("RT_WALK_ANY");
-    if (wa && wa[0] == '1') d->walk_any_env = 1;
-    const char *so = getenv("RT_SOLO");
-    if (so && (so[0] == '0' || so[0] == '1')) d->solo_env = so[0] - '0';
+    if (const int rc = apply_options(d, options)) {
+        rt_device_destroy(d);
+        return rc;
+    }
+    // diagnostic hooks only (the -DRTK_STATS build's counters, per-wave timestamps): what is
+    // computed, and how, is fixed by the options
     const char *wt = getenv("RT_WAVETIMES");
     d->want_wave_times = wt && wt[0] == '1';
-    const char *lp = getenv("RT_LANES_PER_PIXEL");  // 1, 2 or 4 (A/B of the work shape)
-    if (lp) {
-        const int v = atoi(lp);
-        d->lanes_per_pixel = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
-    }
-    const char *mr = getenv("RT_MERGE_ROUNDS");
-    if (mr && (mr[0] == '0' || mr[0] == '1')) d->merge_env = mr[0] - '0';
-    const char *psort = getenv("RT_PIXEL_SORT");
-    if (psort && (psort[0] == '0' || psort[0] == '1')) d->pixel_sort_env = psort[0] - '0';
-    const char *cps = getenv("RT_CUR_PASS");
-    if (cps && (cps[0] == '0' || cps[0] == '1')) d->cur_pass = (uint32_t)(cps[0] - '0');
-    const char *xg = getenv("RT_XCD_GROUP");
-    if (xg && (xg[0] == '0' || xg[0] == '1')) d->xcd_group_env = xg[0] - '0';
-    const char *pseg = getenv("RT_PIXEL_SEG");
-    if (pseg && (pseg[0] == '1' || pseg[0] == '2' || pseg[0] == '4')) d->pixel_seg = (uint32_t)(pseg[0] - '0');
-    const char *ppl = getenv("RT_PIXELS_PER_LANE");
-    if (ppl && (ppl[0] == '1' || ppl[0] == '4')) d->pixels_per_lane_env = ppl[0] - '0';
     const char *st = getenv("RT_STATS");
     if (st && st[0] == '1' && hipMalloc(&d->d_stats, kStatSlots * sizeof(unsigned long long)) == hipSuccess)
         (void)hipMemset(d->d_stats, 0, kStatSlots * sizeof(unsigned long long));
@@ -465,9 +487,10 @@ static bool prefilter_rows(std::vector<float> &gv, uint32_t n_groups, bool simd)
 //   cluster  -(max_j ((delta_j + r_j)(1 + 2^-15) + 4.3u delta_j) + 4.3u),
 //   member   -(r_j (1 + 2^-15) + 4.3u),
 // and a lane's behind test is T < RN(stored - 4.5u cc).
+// k_override / sub_override: rt_device_options ClusterCount / SubClusterSpheres (0: per scene, below).
 static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, std::vector<float> &tab,
                               uint32_t *words, bool relative = false, uint32_t *levels = nullptr,
-                              uint32_t *sub_pairs = nullptr) {
+                              uint32_t *sub_pairs = nullptr, uint32_t k_override = 0, uint32_t sub_override = 0) {
     if (levels) *levels = 0;
     if (sub_pairs) *sub_pairs = 0;
     tab.clear();
@@ -517,7 +540,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     const bool two_levels = *words >= 2u;
     const uint32_t div = two_levels ? (relative ? 17u : 10u) : (relative ? 12u : 8u);
     uint32_t k = std::max(2u, std::max((uint32_t)std::lround(1.25 * std::sqrt((double)n)), n / div));
-    if (const char *ek = getenv("RT_CLUSTER_K")) k = std::min(n, std::max(2u, (uint32_t)atoi(ek)));  // A/B knob
+    if (k_override) k = std::min(n, std::max(2u, k_override));  // A/B (rt_device_options ClusterCount)
     // k-means (f64, fixed LCG restarts) of the spheres idx into k clusters,
     // minimising the sum of rho_c^2; returns each sphere's label
     uint64_t lcg = 0x9E3779B97F4A7C15ull;
@@ -699,7 +722,7 @@ static uint32_t cluster_table(const std::vector<float> &gv, uint32_t n_groups, s
     // pair entries contiguous per top cluster, padded to whole pairs.
     const bool two = two_levels;
     uint32_t sub_spheres = relative ? 4u : 3u;
-    if (const char *es = getenv("RT_SUB_SPHERES")) sub_spheres = std::max(1u, (uint32_t)atoi(es));  // A/B knob
+    if (sub_override) sub_spheres = sub_override;  // A/B (rt_device_options SubClusterSpheres)
     std::vector<std::vector<Cl>> sub(cl.size());
     if (two)
         for (size_t c = 0; c < tops.size(); ++c) {
@@ -839,7 +862,8 @@ struct PackedSet {
     uint32_t cl_levels = 0, cl_sub_pairs = 0;  // two-level tables (cl_words >= 2)
 };
 
-static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env = -1) {
+static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env = -1, uint32_t cluster_k = 0,
+                    uint32_t sub_spheres = 0) {
     const uint32_t ng = scene->SIMDSpheres.Count;
     const uint32_t ns = scene->ScalarSpheres.Count;
     if (ng == 0 || !scene->SIMDSpheres.Data || !scene->Materials.Data || ns == 0 || !scene->ScalarSpheres.Data)
@@ -892,7 +916,8 @@ static int pack_set(const rt_scene *scene, int rs, PackedSet &p, int pf_rel_env 
     // (rt_kernel.hip kPfRel, kClRel): the cluster table is built for that rule, and
     // row 3 then holds r^2 (-inf: never hit).
     p.relative = pf_rel_env == 1 || (pf_rel_env < 0 && !p.prefilter_pays);
-    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words, p.relative, &p.cl_levels, &p.cl_sub_pairs);
+    p.n_cpairs = cluster_table(gv, n, p.clusters, &p.cl_words, p.relative, &p.cl_levels, &p.cl_sub_pairs, cluster_k,
+                               sub_spheres);
     if (p.relative)
         for (uint32_t sl = 0; sl < 4u * n; ++sl) {
             const size_t base = (size_t)(sl / 4u) * 4u * kGroupF4 + sl % 4u;
@@ -906,7 +931,7 @@ extern "C" int rt_scene_upload(rt_device *d, const rt_scene *scene) {
     if (!d || !scene) return fail(RT_EINVAL, "rt_scene_upload: NULL argument");
     PackedSet ps[2];
     for (int rs = 0; rs < 2; ++rs) {
-        const int rc = pack_set(scene, rs, ps[rs], d->pf_rel_env);
+        const int rc = pack_set(scene, rs, ps[rs], d->pf_rel_env, d->cluster_k, d->sub_spheres);
         if (rc) return rc;
     }
     HIP_OK(hipSetDevice(d->ordinal));
@@ -1328,6 +1353,10 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             }
         } else {
             HIP_OK(hipMemsetAsync(d->d_tile_cost, 0, n_units * 4u, s));
+            // no cull pass: every block tile is live, and the totals word the XCD grouping reads
+            // (rtk_launch_xcd_group) says so (u64 little-endian: low word n_tiles, the rest 0)
+            HIP_OK(hipMemsetAsync(d->d_cull_counters + kCullTotals, 0, 2 * sizeof(unsigned long long), s));
+            HIP_OK(hipMemsetD32Async((hipDeviceptr_t)(d->d_cull_counters + kCullTotals), n_tiles, 1, s));
             d->n_live = n_tiles;
             d->dead_pixels = 0;
             d->counts_known = true;

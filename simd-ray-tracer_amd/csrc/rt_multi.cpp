@@ -33,6 +33,9 @@ namespace {
 // ------------------------------------------------------------ RCCL (dlopen)
 struct Rccl {
     bool ok = false;
+    // tests/loopback_rccl's stand-in library (rtLoopbackSharedDevices): its communicators may
+    // list a device twice, which the real RCCL refuses (so with it, never tried)
+    bool shared_devices = false;
     ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
     ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
@@ -68,6 +71,7 @@ const Rccl &rccl() {
     sym(r.GroupEnd, "ncclGroupEnd");
     sym(r.GetErrorString, "ncclGetErrorString");
     r.ok = all;
+    r.shared_devices = dlsym(h, "rtLoopbackSharedDevices") != nullptr;
     return r;
 }
 
@@ -189,6 +193,11 @@ extern "C" int rt_multi_destroy(rt_multi *m) {
 }
 
 extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t transport, rt_multi **out) {
+    return rt_multi_create_ex(hip_devices, count, transport, nullptr, out);
+}
+
+extern "C" int rt_multi_create_ex(const int *hip_devices, uint32_t count, uint32_t transport,
+                                  const rt_device_options *options, rt_multi **out) {
     DeviceGuard device_guard;  // the caller's current device is restored on return
     if (!hip_devices || !out || count == 0 || count > RT_MULTI_MAX_DEVICES)
         return rt_fail(RT_EINVAL, "rt_multi_create: need 1..%u devices", RT_MULTI_MAX_DEVICES);
@@ -199,7 +208,7 @@ extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t 
     for (uint32_t i = 0; i < count; ++i) {
         Shard &sh = m->s[i];
         sh.ordinal = hip_devices[i];
-        int rc = rt_device_create(sh.ordinal, &sh.dev);
+        int rc = rt_device_create_ex(sh.ordinal, options, &sh.dev);
         if (rc) {
             rt_multi_destroy(m);
             return rc;
@@ -233,7 +242,7 @@ extern "C" int rt_multi_create(const int *hip_devices, uint32_t count, uint32_t 
     for (uint32_t i = 0; i < count; ++i)
         for (uint32_t j = 0; j < i; ++j) distinct = distinct && hip_devices[i] != hip_devices[j];
     bool use_rccl = false;
-    if (transport != RT_MULTI_PEER && distinct && rccl().ok) {
+    if (transport != RT_MULTI_PEER && (distinct || rccl().shared_devices) && rccl().ok) {
         std::vector<ncclComm_t> comms(count, nullptr);
         std::vector<int> devs(hip_devices, hip_devices + count);
         if (rccl().CommInitAll(comms.data(), (int)count, devs.data()) == ncclSuccess) {
@@ -373,6 +382,12 @@ extern "C" int rt_multi_reserve(rt_multi *m, uint32_t width, uint32_t height, ui
     if (const int rc = grow(&m->stage_cur, &m->cap_stage_cur, (size_t)n * maxr * width * 4u)) return rc;
     if (flags & RT_MULTI_RESERVE_MEAN)
         if (const int rc = grow(&m->stage_prev, &m->cap_stage_prev, (size_t)n * maxr * width * 16u)) return rc;
+    return RT_OK;
+}
+
+extern "C" int rt_multi_resident_frames(rt_multi *m, uint64_t *out) {
+    if (!m || !out) return rt_fail(RT_EINVAL, "rt_multi_resident_frames: NULL argument");
+    *out = m->accum_valid ? m->resident_frames : 0u;
     return RT_OK;
 }
 

@@ -51,8 +51,40 @@ def pytest_configure(config):
                                              cwd=ROOT, stdout=log, stderr=subprocess.STDOUT)
 
 
+    # rt_multi's RCCL branch over eight shards of this GPU, through the test-only
+    # loopback librccl.so.1 (tests/loopback_rccl, first on LD_LIBRARY_PATH of that
+    # child only); tests/test_gpu_multi.py checks its frames
+    if _selects_gpu(config) and LOOPBACK_BIN.exists():
+        import subprocess
+        if LOOPBACK_OUT.exists():
+            LOOPBACK_OUT.unlink()
+        LOOPBACK_OUT.parent.mkdir(exist_ok=True)
+        env = dict(os.environ)
+        env["LD_LIBRARY_PATH"] = os.pathsep.join(p for p in (str(LOOPBACK_BIN.parent), env.get("LD_LIBRARY_PATH"))
+                                                 if p)
+        log = open(LOOPBACK_OUT.with_suffix(".log"), "w")
+        _loopback["proc"] = subprocess.Popen([str(LOOPBACK_BIN), str(LOOPBACK_OUT), "8"], cwd=ROOT, env=env,
+                                             stdout=log, stderr=subprocess.STDOUT)
+
+
+LOOPBACK_BIN = ROOT / "tests" / "loopback_rccl" / "multi_rccl_check"
+LOOPBACK_OUT = ROOT / "gpurun_out" / "multi_rccl_check.json"
+_loopback = {}
+
+
+@pytest.fixture(scope="session")
+def loopback_rccl_result():
+    """(exit code, JSON) of tests/loopback_rccl/multi_rccl_check (waits for it)."""
+    import json
+    p = _loopback.get("proc")
+    if p is None:
+        pytest.skip("loopback RCCL run not started (run with -m gpu after build())")
+    rc = p.wait(timeout=280)
+    return rc, (json.loads(LOOPBACK_OUT.read_text()) if LOOPBACK_OUT.exists() else None)
+
+
 def pytest_unconfigure(config):
-    for p in [_multirank.get("proc")] + list(_c_host.values()):
+    for p in [_multirank.get("proc"), _loopback.get("proc")] + list(_c_host.values()):
         if p is not None and p.poll() is None:
             try:
                 p.wait(timeout=300)

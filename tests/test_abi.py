@@ -194,3 +194,51 @@ def test_bench_finds_the_fixture_of_each_preset():
     assert bench.golden_for(a, a.width, a.height, a.spp, 64, a.bounces) == (None, None)
     assert bench.combine_verified(None, True) is True and bench.combine_verified(True, False) is False
     assert bench.combine_verified(None, None) is None
+
+
+def test_device_options_are_checked_before_any_device(rt):
+    """rt_device_options (rt_device_create_ex) replaces the environment knobs the
+    library read before round 6: bad values are refused before the call looks
+    for a device (so this runs without one), unknown names never reach C, and a
+    zero-filled struct is rt_device_create's behaviour.  The library reads no
+    environment variable that selects kernels or schedules."""
+    import ctypes
+    with pytest.raises(rt.RtError, match="switch is 5"):
+        rt.Device(0, options={"Cull": 5})
+    with pytest.raises(rt.RtError, match="LanesPerPixel 3"):
+        rt.Device(0, options={"LanesPerPixel": 3})
+    with pytest.raises(rt.RtError, match="count is out of range"):
+        rt.Device(0, options={"SplitParts": 9})
+    with pytest.raises(KeyError, match="unknown device option"):
+        rt.device_options({"RT_CULL": 0})
+    o = rt.RtDeviceOptions()
+    o.Size = 7
+    h = ctypes.c_void_p()
+    assert rt.lib().rt_device_create_ex(0, ctypes.byref(o), ctypes.byref(h)) == -22
+    assert b"Size 7" in rt.lib().rt_last_error()
+    assert rt.parse_options(["Cull=off", "LanesPerPixel=16", "XcdGroup=on", "Prefilter=default"]) == {
+        "Cull": -1, "LanesPerPixel": 16, "XcdGroup": 1, "Prefilter": 0}
+    assert rt.device_options({"Cull": False, "TileOrder": True}).Cull == -1
+    assert ctypes.sizeof(rt.RtDeviceOptions) == 4 * (1 + len(rt.OPTION_FIELDS))
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "--undefined-only", str(rt.LIB_PATH)], capture_output=True, text=True).stdout
+    assert "getenv" in syms  # the diagnostic hooks (RT_STATS, RT_WAVETIMES) only:
+    src = (ROOT / "simd-ray-tracer_amd" / "csrc" / "rt_host.cpp").read_text()
+    names = re.findall(r'getenv\("(\w+)"\)', src)
+    assert sorted(names) == ["RT_STATS", "RT_WAVETIMES"], names
+    for f in (ROOT / "simd-ray-tracer_amd" / "csrc").glob("*"):
+        if f.name != "rt_host.cpp" and f.suffix in (".cpp", ".hip", ".h"):
+            assert "getenv" not in f.read_text(), f.name
+
+
+def test_code_object_hash_reads_the_fatbin(rt, tmp_path):
+    """The binary hash bench.py ties PMC records to: the .hip_fatbin section
+    of the library (stable across a host-only relink, moved by any kernel
+    change); a file without the section is refused."""
+    h = rt.code_object_hash()
+    assert len(h) == 16 and int(h, 16) >= 0
+    assert rt.code_object_hash(rt.LIB_PATH) == h
+    bad = tmp_path / "x.so"
+    bad.write_bytes(b"not an elf")
+    with pytest.raises(rt.RtError, match="ELF64"):
+        rt.code_object_hash(bad)

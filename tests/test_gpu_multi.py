@@ -339,3 +339,60 @@ def test_multi_reserve_that_grows_the_mean_refuses_a_continuation(rt, orc, torch
     oprev, ocur, _ = orc.render(o, orc.camera(o, W, H), W, H, frames=3, max_bounce=B)
     assert np.array_equal(got[0].cpu().numpy().view(np.uint32).reshape(-1, 4), oprev.view(np.uint32))
     assert np.array_equal(got[1].cpu().numpy().view(np.uint32), ocur)
+
+
+def test_on_render_multi_reserve_after_the_first_frame_restarts(rt, orc, torch_cuda):
+    """with several devices, a reservation that grows the shards
+    right after frame 0 (PreviousRayCount still 0) drops the resident means;
+    the next OnRender call must restart the mean instead of continuing it
+    (which rt_multi_trace refuses).  The frames handed out are the oracle's:
+    the completed frame 0, the restarted frame 0, then frames 1 and 2."""
+    rt.on_init(devices=[0, 0])
+    try:
+        W, H = 64, 48
+        img = np.zeros((H, W), np.uint32)
+        o = orc.scene_builtin(1)
+        ocam = orc.camera(o, W, H)
+        done, _, _ = rt.on_render(img, 1)
+        assert not done
+        rt.on_render_wait()
+        rt.on_render_reserve(1920, 1088)  # past OnInit's 1280x720: the shards' means grow (and are dropped)
+        got = []
+        for _ in range(4):
+            done, _, _ = rt.on_render(img, 1)
+            assert done
+            got.append(img.copy())
+            rt.on_render_wait()
+    finally:
+        rt.on_shutdown()
+    for k, frames in enumerate((1, 1, 2, 3)):
+        _, ocur, _ = orc.render(o, ocam, W, H, frames=frames, max_bounce=5)
+        assert np.array_equal(got[k].reshape(-1), ocur), k
+
+
+def test_rccl_branch_over_eight_shards_of_one_gpu(loopback_rccl_result, rt):
+    """rt_multi's RCCL transport (grouped ncclSend/ncclRecv of every shard's
+    band image, running mean and ray count to devices[0], transfer streams, the
+    two band-image slots and their sent events; main.cpp:851-856 /
+    wasm/wasm.cpp:651-678's gather) over eight shards of this GPU, through the
+    test-only loopback librccl.so.1 (tests/loopback_rccl: RCCL's point-to-point
+    semantics as stream-ordered copies; the real RCCL refuses a device listed
+    twice).  tests/loopback_rccl/multi_rccl_check, started by conftest before
+    this process touched the GPU, traces BASELINE C2 (1920x1080, 256 spp, 64
+    spheres, 8 bounces) with the gathered mean, an 8-frame continuation on the
+    resident means and three restarts back to back, each compared byte for byte
+    with one device's whole-frame render; C2's hashes and ray count must be the
+    golden's (rendered by the reference itself).  rt_comm with several
+    processes stays untested on a one-GPU box."""
+    import json
+    import pathlib
+    rc, out = loopback_rccl_result
+    assert out is not None and rc == 0, (rc, out)
+    assert out["transport"] == "rccl" and out["devices"] == 8
+    gold = json.loads((pathlib.Path(__file__).parent / "golden" / "oracle_regression.json").read_text())
+    g = gold["c2_full_1920x1080x256"]
+    a = out["a"]
+    assert a["equal_one_device"] and a["rays"] == g["rays"] == 719275410
+    assert a["fnv1a64_rgba8"] == g["fnv1a64_rgba8"] and a["fnv1a64_v4"] == g["fnv1a64_v4"]
+    assert out["b"]["equal_one_device"] and out["b"]["resident_frames"] == 264
+    assert out["c"]["equal_one_device"] == [True, True, True] and out["c"]["resident_frames"] == 3004

@@ -131,22 +131,18 @@ def test_one_frame_launches_take_four_pixels_per_lane(rt, orc, torch_cuda, gdev,
             assert np.array_equal(g[1].cpu().numpy().view(np.uint32), oc), (r, k)
 
 
-@pytest.mark.parametrize("order,xcd,seg", [("1", "1", "1"), ("1", "0", "1"), ("0", "1", "1"), ("1", "1", "2"),
-                                            ("1", "1", "4")])
-@pytest.mark.parametrize("scene_idx,n,W,H,spp,B,lpp", [(1, 64, 96, 80, 8, 8, "4"), (2, None, 72, 56, 8, 5, "4"),
-                                                       (0, None, 64, 48, 16, 5, "8"), (1, 200, 40, 32, 16, 8, "16")])
-def test_pixels_dealt_by_cost_keep_every_bit(rt, orc, torch_cuda, monkeypatch, scene_idx, n, W, H, spp, B, lpp,
-                                             order, xcd, seg):
-    """RT_PIXEL_SORT=1: after a launch measures each pixel's traced segments,
+@pytest.mark.parametrize("order,xcd,seg", [(1, 1, 1), (1, -1, 1), (-1, 1, 1), (1, 1, 2), (1, 1, 4)])
+@pytest.mark.parametrize("scene_idx,n,W,H,spp,B,lpp", [(1, 64, 96, 80, 8, 8, 4), (2, None, 72, 56, 8, 5, 4),
+                                                       (0, None, 64, 48, 16, 5, 8), (1, 200, 40, 32, 16, 8, 16)])
+def test_pixels_dealt_by_cost_keep_every_bit(rt, orc, torch_cuda, scene_idx, n, W, H, spp, B, lpp, order, xcd, seg):
+    """PixelSort on: after a launch measures each pixel's traced segments,
     every block tile's pixels are dealt to its four waves cheapest first (and
     a permuted wave tests the union of the block's quadrant masks).  Repeated
     launches with the permutation in place equal the oracle bit for bit."""
-    monkeypatch.setenv("RT_PIXEL_SORT", "1")
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", lpp)
-    monkeypatch.setenv("RT_WAVE_ORDER", order)  # waves ordered by cost, or block tiles
-    monkeypatch.setenv("RT_XCD_GROUP", xcd)  # a block tile's waves grouped onto one XCD (wave order only)
-    monkeypatch.setenv("RT_PIXEL_SEG", seg)  # pixels dealt singly, in pairs or in 4-pixel row segments
-    dev = rt.Device(0)
+    dev = rt.Device(0, options={"PixelSort": rt.RT_OPT_ON, "LanesPerPixel": lpp,
+                                "WaveOrder": order,  # waves ordered by cost, or block tiles
+                                "XcdGroup": xcd,  # a block tile's waves grouped onto one XCD (wave order only)
+                                "PixelSegment": seg})  # pixels dealt singly, in pairs or in 4-pixel row segments
     try:
         s, o = _scenes(rt, orc, scene_idx, n)
         cam = rt.camera_setup(s, W, H)
@@ -374,37 +370,43 @@ def test_on_render_moving_camera_restarts_every_frame(rt, orc, torch_cuda):
         rt.on_shutdown()
 
 
-# Kernel variants selected at device creation (rt_host.cpp reads the env):
-# prefilter forced on/off, brute-force primaries, 1/2/16/32 lanes per pixel, the
-# LDS-staged sphere source, four-wave workgroups, the run-time walk dispatch.
-# Every variant must give the same bits as the oracle.
-VARIANT_ENVS = [{"RT_PREFILTER": "1"}, {"RT_PREFILTER": "0"}, {"RT_CLUSTERS": "0"}, {"RT_CLUSTERS": "2"},
-                {"RT_INTERLEAVE": "1"}, {"RT_CULL": "0"}, {"RT_LANES_PER_PIXEL": "1"}, {"RT_LANES_PER_PIXEL": "2"},
-                {"RT_LANES_PER_PIXEL": "32"}, {"RT_SEC_THRESHOLD": "1"}, {"RT_SPHERE_SRC": "lds"},
-                {"RT_SPHERE_SRC": "lds", "RT_CULL": "0"}, {"RT_SPHERE_SRC": "lds", "RT_CLUSTERS": "0"},
-                {"RT_SCENE_GLOBAL": "1"}, {"RT_SCENE_GLOBAL": "1", "RT_CULL": "0"},
-                # four-wave workgroups with the LDS image (the default is one wave per
-                # workgroup, each kernel compiled for one secondary walk)
-                {"RT_SOLO": "0"}, {"RT_SOLO": "0", "RT_CLUSTERS": "2"}, {"RT_WALK_ANY": "1"},
-                {"RT_WALK_ANY": "1", "RT_CLUSTERS": "2"}, {"RT_LANES_PER_PIXEL": "16", "RT_CLUSTERS": "2"},
-                # 4 pixels per lane at every frame count (the one-frame launch shape), and never
-                {"RT_LANES_PER_PIXEL": "1", "RT_PIXELS_PER_LANE": "4"}, {"RT_PIXELS_PER_LANE": "1"},
-                # merged primary/secondary rounds forced on (every per-group-walk kernel) and off
-                {"RT_MERGE_ROUNDS": "1", "RT_CLUSTERS": "0"}, {"RT_MERGE_ROUNDS": "0"}, {"RT_PIXEL_SORT": "0"},
-                # block tiles ordered by cost instead of waves
-                {"RT_WAVE_ORDER": "0"},
-                # round 5: RGBA8 stored by the trace kernel (no encode pass); pixel pairs / 4-pixel
-                # row segments dealt by cost; waves not grouped by XCD
-                {"RT_CUR_PASS": "0"}, {"RT_PIXEL_SEG": "2"}, {"RT_PIXEL_SEG": "4"}, {"RT_XCD_GROUP": "0"}]
+# Kernel variants selected at device creation through the C-ABI (rt_device_options,
+# rt_device_create_ex; 1 = RT_OPT_ON, -1 = RT_OPT_OFF): prefilter forced on/off,
+# brute-force primaries, 1/2/16/32 lanes per pixel, the LDS-staged sphere source,
+# four-wave workgroups, the run-time walk dispatch.  Every variant must give the
+# same bits as the oracle.
+ON, OFF = 1, -1
+VARIANT_OPTIONS = [{"Prefilter": ON}, {"Prefilter": OFF}, {"Clusters": OFF}, {"Clusters": ON},
+                   {"Interleave": ON}, {"Cull": OFF}, {"LanesPerPixel": 1}, {"LanesPerPixel": 2},
+                   {"LanesPerPixel": 32}, {"SecondaryThreshold": 1}, {"SphereSourceLds": ON},
+                   {"SphereSourceLds": ON, "Cull": OFF}, {"SphereSourceLds": ON, "Clusters": OFF},
+                   {"SceneInHbm": ON}, {"SceneInHbm": ON, "Cull": OFF},
+                   # four-wave workgroups with the LDS image (the default is one wave per
+                   # workgroup, each kernel compiled for one secondary walk)
+                   {"OneWaveGroups": OFF}, {"OneWaveGroups": OFF, "Clusters": ON}, {"WalkAny": ON},
+                   {"WalkAny": ON, "Clusters": ON}, {"LanesPerPixel": 16, "Clusters": ON},
+                   # 4 pixels per lane at every frame count (the one-frame launch shape), and never
+                   {"LanesPerPixel": 1, "PixelsPerLane": 4}, {"PixelsPerLane": 1},
+                   # merged primary/secondary rounds forced on (every per-group-walk kernel) and off
+                   {"MergeRounds": ON, "Clusters": OFF}, {"MergeRounds": OFF}, {"PixelSort": OFF},
+                   # block tiles ordered by cost instead of waves
+                   {"WaveOrder": OFF},
+                   # round 5: RGBA8 stored by the trace kernel (no encode pass); pixel pairs / 4-pixel
+                   # row segments dealt by cost; waves not grouped by XCD
+                   {"EncodePass": OFF}, {"PixelSegment": 2}, {"PixelSegment": 4}, {"XcdGroup": OFF},
+                   # round 6: the brute-force roofline's kernel (bench.py --brute), the XCD grouping
+                   # without the cull pass (its live-tile total written by the host), the cluster
+                   # table's K and sub-cluster size
+                   {"Cull": OFF, "Prefilter": OFF}, {"Cull": OFF, "XcdGroup": ON},
+                   {"ClusterCount": 3, "SubClusterSpheres": 2}]
 
 
-@pytest.mark.parametrize("env", VARIANT_ENVS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
-def test_kernel_variants_match_oracle(rt, orc, torch_cuda, monkeypatch, env):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    dev = rt.Device(0)
+@pytest.mark.parametrize("options", VARIANT_OPTIONS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_kernel_variants_match_oracle(rt, orc, torch_cuda, options):
+    dev = rt.Device(0, options=options)
+    assert dev.options() == options
     try:
-        # (1, 200): 50 groups, the two-word cluster mask under RT_CLUSTERS=2
+        # (1, 200): 50 groups, the two-word cluster mask with Clusters on
         for scene_idx, n, W, H, spp, B in [(1, 64, 64, 48, 6, 8), (1, 200, 40, 32, 3, 8), (0, None, 48, 32, 4, 5),
                                            (2, None, 40, 24, 2, 5)]:
             for simd in (True, False):
@@ -443,47 +445,41 @@ def test_tiny_sphere_scene_takes_the_ieee_sqrt(rt, orc, torch_cuda, gdev):
 
 
 @pytest.mark.parametrize("scene_idx,n", [(1, 64), (1, 256), (0, None)])
-def test_cone_culling_is_exact_at_full_resolution(rt, orc, torch_cuda, monkeypatch, scene_idx, n):
+def test_cone_culling_is_exact_at_full_resolution(rt, orc, torch_cuda, scene_idx, n):
     """Primary-ray cone culling (tight f64 cones, per 4x4 / 2x2 tile) and the
     empty-tile fast path must not change a single bit at the BASELINE
-    resolution: the culled kernel against the brute-force one (RT_CULL=0),
+    resolution: the culled kernel against the brute-force one (Cull off),
     full 1920x1080 frame, several lanes-per-pixel shapes."""
     s, _ = _scenes(rt, orc, scene_idx, n)
     W, H = 1920, 1080
     cam = rt.camera_setup(s, W, H)
     out = {}
-    for env in ({"RT_CULL": "0", "RT_LANES_PER_PIXEL": "4"}, {"RT_LANES_PER_PIXEL": "4"},
-                {"RT_LANES_PER_PIXEL": "16"}, {"RT_LANES_PER_PIXEL": "1"}):
-        monkeypatch.delenv("RT_CULL", raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        dev = rt.Device(0)
+    for opts in ({"Cull": OFF, "LanesPerPixel": 4}, {"LanesPerPixel": 4}, {"LanesPerPixel": 16},
+                 {"LanesPerPixel": 1}):
+        dev = rt.Device(0, options=opts)
         try:
-            out[tuple(env.items())] = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=3, bounces=8)
+            out[tuple(opts.items())] = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=3, bounces=8)
         finally:
             dev.close()
-    ref = out[(("RT_CULL", "0"), ("RT_LANES_PER_PIXEL", "4"))]
+    ref = out[(("Cull", OFF), ("LanesPerPixel", 4))]
     for key, g in out.items():
         assert torch_cuda.equal(g[0], ref[0]) and torch_cuda.equal(g[1], ref[1]) and g[2] == ref[2], key
 
 
-@pytest.mark.parametrize("lpp", ["4", "16", "32"])
-def test_tile_order_from_previous_launch_keeps_every_bit(rt, orc, torch_cuda, monkeypatch, lpp):
+@pytest.mark.parametrize("lpp", [4, 16, 32])
+def test_tile_order_from_previous_launch_keeps_every_bit(rt, orc, torch_cuda, lpp):
     """Repeated launches of one geometry run their tiles heaviest-first (order
     learned from the previous launch): the image, the accumulation and the ray
     count must equal the identity-order launch bit for bit, launch after launch."""
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", lpp)
     s, _ = _scenes(rt, orc, 1, 64)
     W, H = 640, 360
     cam = rt.camera_setup(s, W, H)
-    monkeypatch.setenv("RT_TILE_ORDER", "0")
-    dev0 = rt.Device(0)
+    dev0 = rt.Device(0, options={"LanesPerPixel": lpp, "TileOrder": OFF})
     try:
         ref = gpu_render(rt, torch_cuda, dev0, s, cam, W, H, frames=6, bounces=8)
     finally:
         dev0.close()
-    monkeypatch.setenv("RT_TILE_ORDER", "1")
-    dev = rt.Device(0)
+    dev = rt.Device(0, options={"LanesPerPixel": lpp, "TileOrder": ON})
     try:
         for _ in range(4):
             g = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=6, bounces=8)
@@ -509,21 +505,20 @@ def test_dead_tiles_fold_a_nonzero_running_mean(rt, orc, torch_cuda, gdev):
 
 @pytest.mark.parametrize("prev_count,P", [(65533, 4), (65530, 16), (1000003, 4), (16777217, 16), (300000001, 1),
                                           (4294967000, 8)])
-def test_running_mean_weights_at_large_previous_counts(rt, orc, torch_cuda, monkeypatch, prev_count, P):
+def test_running_mean_weights_at_large_previous_counts(rt, orc, torch_cuda, prev_count, P):
     """The fold weights RN(1/(f32)(n)) and RN((f32)(n-1)/(f32)(n)) (main.cpp:484-487)
     come from the device's static table of the first 65,536 frames (TraceArgs.weights)
     and past it from rcp_rn / div_rn (rt_kernel.hip fold_weights) in the one-wave
     kernels: launches across the table's end, frames far past it, counts whose f32
     conversion rounds (> 2^24) and the top of the u32 range, against the oracle's IEEE
     divisions, with a random non-zero running mean, every lane shape's blend path."""
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", str(P))
     s, o = _scenes(rt, orc, 1, 64)
     W, H = 64, 48
     cam = rt.camera_setup(s, W, H)
     rng = np.random.default_rng(prev_count % 1000)
     prev_np = rng.uniform(0.0, 2.0, (W * H, 4)).astype(np.float32)
     prev = torch_cuda.from_numpy(prev_np.copy()).to("cuda")
-    dev = rt.Device(0)
+    dev = rt.Device(0, options={"LanesPerPixel": P})
     try:
         g = gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=P, bounces=4, prev_count=prev_count, prev=prev)
     finally:
@@ -545,7 +540,7 @@ def test_camera_change_recomputes_the_cull_pass(rt, orc, torch_cuda, gdev):
 
 
 @pytest.mark.parametrize("simd", [True, False])
-def test_new_cameras_back_to_back_without_host_sync(rt, orc, torch_cuda, monkeypatch, simd):
+def test_new_cameras_back_to_back_without_host_sync(rt, orc, torch_cuda, simd):
     """Three different cameras enqueued back to back with no synchronisation in
     between: each is a new cull key whose live-tile count stays
     on the device (grid over every tile, early exit), and its dead-tile segments
@@ -557,8 +552,7 @@ def test_new_cameras_back_to_back_without_host_sync(rt, orc, torch_cuda, monkeyp
     s, o = _scenes(rt, orc, 1, 64)
     W, H, F, B = 160, 96, 128, 5
     views = [(None, None), (6.0, 0.7), (2.0, -1.1)]
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", "4")  # P = 4: a 128-frame launch is split (head + rest)
-    dev = rt.Device(0)
+    dev = rt.Device(0, options={"LanesPerPixel": 4})  # P = 4: a 128-frame launch is split (head + rest)
     try:
         dev.upload_scene(s)
         stream = torch.cuda.current_stream().cuda_stream
@@ -614,17 +608,16 @@ def test_stream_switch_keeps_every_bit(rt, orc, torch_cuda):
 
 @pytest.mark.parametrize("idx,n,W,H,P", [(1, 64, 96, 64, 4), (1, 128, 16, 16, 1), (1, 200, 40, 32, 2),
                                          (1, 256, 64, 48, 8), (0, None, 48, 32, 16)])
-def test_cull_masks_equal_cpu_restatement(rt, torch_cuda, monkeypatch, idx, n, W, H, P):
+def test_cull_masks_equal_cpu_restatement(rt, torch_cuda, idx, n, W, H, P):
     """The cull pass's primary group masks (rt_debug_masks) equal the numpy f64
     restatement (tests/cull_ref.py) word for word; tests/test_cull_bound.py
     checks that restatement keeps every group a pixel's rays can reach."""
     from cull_ref import np_masks
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", str(P))
     s = rt.scene_builtin(idx)
     if n:
         s = rt.scene_prefix(s, n)
     cam = rt.camera_setup(s, W, H)
-    dev = rt.Device(0)
+    dev = rt.Device(0, options={"LanesPerPixel": P})
     try:
         gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=1, bounces=1)
         got = dev.debug_masks()
@@ -670,14 +663,13 @@ def test_encode_rgba8_exhaustive(rt, orc, torch_cuda):
 
 
 @pytest.mark.parametrize("n_groups", [164, 265])
-def test_largest_scene_the_lds_image_holds(rt, orc, torch_cuda, gdev, monkeypatch, n_groups):
+def test_largest_scene_the_lds_image_holds(rt, orc, torch_cuda, n_groups):
     """164 groups (656 spheres) is the LDS-staged maximum of the four-wave
     kernels (rt_kernel.h kMaxLdsGroups, 64-B sphere records); 265 groups stay
     in HBM.  RTWeekend's 482 spheres plus (or, at 164 groups, minus) small
     spheres scattered over its ground (materials copied from RTWeekend's),
     both rule sets, traced by the four-wave kernels that stage the image."""
-    monkeypatch.setenv("RT_SOLO", "0")
-    gdev = rt.Device(0)
+    gdev = rt.Device(0, options={"OneWaveGroups": OFF})
     base = rt.scene_builtin(2)
     sp0, _, _ = rt.scene_arrays(base)
     rng = np.random.default_rng(265)
@@ -785,15 +777,14 @@ def test_scene_above_the_limit_is_refused(rt, torch_cuda, gdev):
 
 
 @pytest.mark.parametrize("simd", [True, False], ids=["simd", "scalar"])
-def test_first_launch_split_changes_no_bit(rt, orc, torch_cuda, monkeypatch, simd):
+def test_first_launch_split_changes_no_bit(rt, orc, torch_cuda, simd):
     """The first launch of a key (frames >= 32 P) runs split: a head of 8 samples
     per lane in the cull pass's order, which measures the tile costs, then the
-    rest heaviest-first, continuing the running mean (and with RT_SPLIT_PARTS=3
+    rest heaviest-first, continuing the running mean (and with SplitParts 3
     a second leading part of 8 per lane).  The frame, the accumulation and the
-    ray count equal the unsplit launch's (RT_PROBE=0) and the oracle's -- also
+    ray count equal the unsplit launch's (SplitFirstLaunch off) and the oracle's -- also
     continuing a resident mean (PreviousRayCount > 0) and with
     RT_FLAG_ACCUM_ZERO over a stale buffer."""
-    monkeypatch.setenv("RT_LANES_PER_PIXEL", "4")
     s, o = _scenes(rt, orc, 1, 64)
     W, H, S, B = 192, 128, 128, 8
     cam = rt.camera_setup(s, W, H)
@@ -802,11 +793,9 @@ def test_first_launch_split_changes_no_bit(rt, orc, torch_cuda, monkeypatch, sim
     cases = [("plain", 0, None, False), ("continued", 7, base[0], False), ("accum_zero", 7, base[0], True)]
     for name, pc, prev0, az in cases:
         out, heads = [], []
-        for probe, parts in (("0", "2"), ("1", "2"), ("1", "3")):
-            monkeypatch.setenv("RT_PROBE", probe)
-            monkeypatch.setenv("RT_SPLIT_PARTS", parts)
-            monkeypatch.setenv("RT_SPLIT_GROWTH", "1")
-            dev = rt.Device(0)
+        for probe, parts in ((OFF, 2), (ON, 2), (ON, 3)):
+            dev = rt.Device(0, options={"LanesPerPixel": 4, "SplitFirstLaunch": probe, "SplitParts": parts,
+                                        "SplitGrowth": 1})
             try:
                 prev = None if prev0 is None else torch_cuda.from_numpy(prev0.reshape(-1, 4).copy()).cuda()
                 out.append(gpu_render(rt, torch_cuda, dev, s, cam, W, H, frames=S, bounces=B, simd=simd,
