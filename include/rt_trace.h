@@ -220,7 +220,7 @@ int rt_rsqrt_table_capture_host(float table_out[2048]);
  * HBM: SIMDSpheres/Materials for the SIMD rules, ScalarSpheres for the
  * scalar rules.  The scene is copied; the caller keeps ownership.  The
  * default one-wave kernels read every scene from HBM through the caches; the
- * four-wave kernels (RT_SOLO=0) also stage scenes of up to 656 spheres (164
+ * four-wave kernels (rt_device_options OneWaveGroups off) also stage scenes of up to 656 spheres (164
  * groups) in each block's LDS.  Up to RT_MAX_SPHERES.
  * RT_EINVAL for a scene with no spheres (every built-in scene has some) or
  * more than RT_MAX_SPHERES. */
@@ -300,7 +300,7 @@ typedef struct rt_trace_info {
                                  per-pixel launches of one frame), else 1     */
     uint32_t PixelsSorted;    /* 1: the block tiles' pixels were dealt to their
                                  waves by the previous launch's costs (P >= 4;
-                                 RT_PIXEL_SORT=0 disables)                   */
+                                 PixelSort off disables)                      */
     uint32_t BufferGrowths;   /* launch-buffer (re)allocations on this device
                                  so far (tile lists, cull masks): constant
                                  across launches that rt_device_reserve covers */

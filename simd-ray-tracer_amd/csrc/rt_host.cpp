@@ -31,65 +31,65 @@ struct rt_device {
     bool use_sky = false;
     int src = kSrcSmem;
     int cull = 1;
-    uint32_t sec_threshold = 0;  // 0: per scene (rt_trace), else RT_SEC_THRESHOLD
-    int prefilter_env = -1;  // RT_PREFILTER: -1 auto, 0 off, 1 on
+    uint32_t sec_threshold = 0;  // 0: per scene (rt_trace), else rt_device_options SecondaryThreshold
+    int prefilter_env = -1;  // options Prefilter: -1 auto, 0 off, 1 on
     uint32_t prefilter[2] = {0, 0};  // per rule set, decided at upload
     uint32_t pf_relative[2] = {0, 0};  // per rule set: row 3 holds r^2, per-lane thresholds (rt_kernel.hip kPfRel)
-    int pf_rel_env = -1;  // RT_PF_REL: -1 auto (relative where the scene-wide bound does not pay), 0 never, 1 always
+    int pf_rel_env = -1;  // options PrefilterRelative: -1 auto (where the scene-wide bound does not pay), 0 never, 1 always
     uint32_t fast_sqrt[2] = {0, 0};  // per rule set: candidate sqrt in sqrt_rn's verified range
     float4 *d_clusters[2] = {nullptr, nullptr};  // clustered prefilter tables (cluster_table)
     size_t cap_clusters[2] = {0, 0};             // float4 capacity
     uint32_t n_cpairs[2] = {0, 0};               // 0: per-group prefilter loop
     uint32_t cl_words[2] = {0, 0};
-    // RT_CLUSTERS=0: per-group prefilter loop only; 2: clustered loop up to
+    // options Clusters off (0): per-group prefilter loop only; on (2): clustered loop up to
     // kClMaxGroups groups; default 1: up to kClAutoGroups (measured: clusters
     // win 13-15 % at 16/24/32 groups on C2 geometry, and at C5's 64 groups
     // 32.4k against 28.6k Mrays/s once the behind rule and the 7-block LDS
     // image are in)
     int clusters_env = 1;
-    int interleave_env = 0;  // RT_INTERLEAVE=1: wave tiles interleaved over the block tile (P >= 2)
-    int scene_global_env = 0;  // RT_SCENE_GLOBAL=1: keep the scene in HBM even when the LDS image could hold it
-    int tables_global_env = 0;  // RT_TABLES_LDS=0: the rsqrt and fold-weight tables stay out of the LDS image
-    int solo_env = 1;           // RT_SOLO=0: four waves per workgroup sharing an LDS image (TraceArgs.solo)
-    int wave_order_env = 1;     // RT_WAVE_ORDER=0: one-wave kernels order block tiles, not waves (A/B)
-    int walk_any_env = 0;       // RT_WALK_ANY=1: the one-wave kernel dispatches the walk at run time (A/B)
-    int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by RT_LANES_PER_PIXEL
-    // RT_PIXELS_PER_LANE: 0 auto (4 pixels per lane for one-lane-per-pixel launches of one
+    int interleave_env = 0;  // options Interleave: wave tiles interleaved over the block tile (P >= 2)
+    int scene_global_env = 0;  // options SceneInHbm: keep the scene in HBM even when the LDS image could hold it
+    int tables_global_env = 0;  // options TablesInLds off: the rsqrt and fold-weight tables stay out of the LDS image
+    int solo_env = 1;           // options OneWaveGroups off: four waves per workgroup sharing an LDS image (TraceArgs.solo)
+    int wave_order_env = 1;     // options WaveOrder off: one-wave kernels order block tiles, not waves (A/B)
+    int walk_any_env = 0;       // options WalkAny: the one-wave kernel dispatches the walk at run time (A/B)
+    int lanes_per_pixel = 0;  // 0 = auto per launch (rt_trace), else forced by options LanesPerPixel
+    // options PixelsPerLane: 0 auto (4 pixels per lane for one-lane-per-pixel launches of one
     // frame), 1 never, 4 for every one-lane-per-pixel launch (A/B and the parity suite)
     int pixels_per_lane_env = 0;
     // each block tile's pixels dealt to its waves by the cost the last launch
-    // measured (rtk_launch_pixel_sort), at P >= 4; RT_PIXEL_SORT=0 turns it off.
+    // measured (rtk_launch_pixel_sort), at P >= 4; options PixelSort off turns it off.
     // Same box: C2 158.7-159.3k -> 164.6-166.4k Mrays/s, RTWeekend 22.4k -> 23.3k
     int pixel_sort_env = 1;
-    // pixels per dealt unit (TraceArgs.pix_seg), RT_PIXEL_SEG=1/2/4: 4-pixel row segments keep
+    // pixels per dealt unit (TraceArgs.pix_seg), options PixelSegment 1/2/4: 4-pixel row segments keep
     // each wave's stores to whole 64-B runs of the v4 image (HBM writes per launch: C2 20.9 ->
     // 17.5 MB, RTWeekend 80.2 -> 57.3 MB) but deal costs coarser: C2 -2.2 %, RTWeekend -4 %
     // (profiles/r05b_pixel_seg_ab.txt), so single pixels stay the default
     uint32_t pixel_seg = 1;
-    // RT_XCD_GROUP: every wave of a block tile on one XCD (rtk_launch_xcd_group), so its lines'
+    // options XcdGroup: every wave of a block tile on one XCD (rtk_launch_xcd_group), so its lines'
     // partial stores merge in one L2 before they are written back
-    // RT_XCD_GROUP=0/1 forces it off/on; by default it is on for launches of at most 4 lanes per pixel (the
+    // off/on forces it; by default it is on for launches of at most 4 lanes per pixel (the
     // whole frame, where it halves the trace kernel's HBM writes at no cost) and off for the multi-GPU shares
     // (8 and 16 lanes per pixel: small launches, whose partial-line writes are a few MB, and the 8-rank share
     // -2.3 % without it at the final kernel, profiles/r05z6_xcd_group_ab.txt)
     int xcd_group_env = -1;
     // RGBA8 encoded from the running mean by a coalesced pass after the launch (TraceArgs.skip_cur),
     // at P >= 2: trace-kernel HBM writes C2 21.0 -> 15.7 MB, RTWeekend 80.6 -> 54.1 MB, C2 +0.7 %
-    // (profiles/r05e_cur_pass_ab.txt); RT_CUR_PASS=0 stores RGBA8 in the trace kernel
+    // (profiles/r05e_cur_pass_ab.txt); options EncodePass off stores RGBA8 in the trace kernel
     uint32_t cur_pass = 1;
-    int merge_env = -1;  // RT_MERGE_ROUNDS: -1 auto (scenes of at most kMergeGroups groups), 0 never, 1 always
+    int merge_env = -1;  // options MergeRounds: -1 auto (scenes of at most kMergeGroups groups), 0 never, 1 always
     uint8_t *d_pix_perm = nullptr;  // 64 B per block tile (TraceArgs.pix_perm)
     uint32_t *d_pix_cost = nullptr; // per band pixel (TraceArgs.pix_cost)
     size_t pix_perm_cap = 0, pix_cost_cap = 0;
     // heaviest-first tile order learned from the previous launch of the same
-    // geometry (RT_TILE_ORDER=0 disables); launches must be stream-ordered
+    // geometry (options TileOrder off disables); launches must be stream-ordered
     int tile_sched = 1;
     uint32_t n_sorts = 0;             // re-sorts done for the current tile key
-    int split_env = 1;                // RT_PROBE=0: a key's first launch is not split (below)
-    uint32_t head_samples = 8;        // samples per lane of the split's head (RT_HEAD_SAMPLES)
-    uint32_t split_parts = 2;         // launches of a split first launch (RT_SPLIT_PARTS, <= 8)
-    uint32_t split_growth = 3;        // each leading part this many times the previous (RT_SPLIT_GROWTH)
-    // RT_ORDER_LAUNCHES: re-sorts per key before the order is kept.  4 (a key's split first launch
+    int split_env = 1;                // options SplitFirstLaunch off: a key's first launch is not split (below)
+    uint32_t head_samples = 8;        // samples per lane of the split's head (options HeadSamples)
+    uint32_t split_parts = 2;         // launches of a split first launch (options SplitParts, <= 8)
+    uint32_t split_growth = 3;        // each leading part this many times the previous (options SplitGrowth)
+    // options OrderLaunches: re-sorts per key before the order is kept.  4 (a key's split first launch
     // sorts twice, then two more launches): as fast as 6 at steady state on C2 and the 8-rank share,
     // 3 is slower (profiles/r05q_order_launches_ab.txt), and a bench's timed launches are past the
     // sorting ones after two warm-ups
@@ -1305,7 +1305,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     const size_t mask_words = (size_t)n_tiles * 4u * n_words;
     if (cull)
         if (const int rc = ensure_masks(d, mask_words, s, false)) return rc;
-    // pixels dealt to waves by cost (RT_PIXEL_SORT): block tiles of at most 64 pixels
+    // pixels dealt to waves by cost (options PixelSort): block tiles of at most 64 pixels
     const bool pixel_sort = d->pixel_sort_env && sched && lpp >= 4 && !a.interleave;
     if (pixel_sort)
         if (const int rc = ensure_pixel_sort(d, n_tiles, (size_t)desc->Width * local_rows, s, false)) return rc;
@@ -1431,7 +1431,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
             d->tile_order_valid = true;
         }
     }
-    // RT_CUR_PASS: the RGBA8 band image from the running mean the kernels stored (main.cpp:490's
+    // options EncodePass: the RGBA8 band image from the running mean the kernels stored (main.cpp:490's
     // store on its own, the same bits), written by one coalesced pass
     if (a.skip_cur && desc->Frames > 0 &&
         rtk_launch_encode(a.prev, a.cur, (uint64_t)local_rows * desc->Width, (a.flags & kFlagSrgbPow) ? 1u : 0u, s) != 0)

@@ -87,7 +87,7 @@ struct TraceArgs {
     // one-wave kernels (solo): tile_order / tile_cost index WAVES (4 * block tile + quadrant),
     // so the heaviest-first order ranks every wave on its own cost (rt_host.cpp unit_waves)
     uint32_t unit_waves;
-    // optional (RT_PIXEL_SORT): the block tile's pixels dealt to its four waves by cost,
+    // optional (rt_device_options PixelSort): the block tile's pixels dealt to its four waves by cost,
     // cheapest first: pix_perm[64 * tile + NPIX * wave + pl] = the pixel's index in the
     // block tile (row-major, 2TW wide); pix_perm[64 * tile] == 0xFF: not permuted
     const uint8_t *pix_perm;
@@ -105,7 +105,7 @@ struct TraceArgs {
     uint32_t pix_seg;
     // 1: the trace and empty-tile kernels store only the running mean; the RGBA8 image is
     // encoded from it by one coalesced pass after the launch (rtk_launch_encode), so its 4-B
-    // pixels are not written as scattered partial lines from several XCDs (RT_CUR_PASS)
+    // pixels are not written as scattered partial lines from several XCDs (rt_device_options EncodePass)
     uint32_t skip_cur;
     // CULL (required): the primary rounds' group rows, written by the cull pass for its camera
     // (rtk_launch_cull): per group kPrimF4 float4 = {cx[4]}, {cy[4]}, {cz[4]}, {r*r[4]} with
