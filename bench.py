@@ -101,6 +101,9 @@ def parse():
     p.add_argument("--headline-only", action="store_true",
                    help="skip the extra legs after the timed steps (the brute-force roofline leg and the "
                         "distinct-samples leg): the PMC passes and kernel traces record the headline launches only")
+    p.add_argument("--legs", default="distinct,brute",
+                   help="extra legs after the timed steps (1 GPU, whole frame): 'distinct' (the same steps on "
+                        "samples no launch has seen), 'brute' (the brute-force kernel's roofline), both, or 'none'")
     a = p.parse_args()
     if a.config == "onrender":
         return a
@@ -1013,9 +1016,11 @@ def main():
         dev.close()
         return
     legs = {}
-    if world == 1 and bands == 1 and not args.headline_only:
-        legs["distinct"] = distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, opts)
-        if not args.brute and not opts and W * H * S * N <= 2.2 * 1920 * 1080 * 256 * 64:
+    want = set() if args.headline_only else set(args.legs.split(","))
+    if world == 1 and bands == 1:
+        if "distinct" in want:
+            legs["distinct"] = distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, opts)
+        if "brute" in want and not args.brute and not opts and W * H * S * N <= 2.2 * 1920 * 1080 * 256 * 64:
             legs["brute"] = brute_leg(rt, torch, args, scene, cam, W, H, S, N, B, gpu, stream, binary_hash,
                                       lambda o: workload_name(args, W, H, S, N, B, o))
     if rank == 0:

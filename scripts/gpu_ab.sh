@@ -9,6 +9,7 @@
 #   PARITY=1  run the GPU suite under each library build first (stops at the first failure; options
 #             are parity-tested by tests/test_gpu_parity.py's VARIANT_OPTIONS)
 #   STEPS / WARMUP  bench steps (default 10 / 6)
+#   LEGS      bench.py --legs (default none; "distinct" also times the steps on unseen samples)
 # Prints one line per run: round, variant, config, Mrays/s, ms per step, kernel ms, cold ms.
 set -o pipefail
 mkdir -p gpurun_out
@@ -33,13 +34,14 @@ for r in $(seq $ROUNDS); do
       args=$c; [ "$c" = "c2" ] && args=""
       split_variant "$v"
       env "${VENV[@]}" RT_X=0 timeout -k 10 180 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-6} --no-cpu-baseline \
-        --headline-only "${VARGS[@]}" $args \
+        --legs ${LEGS:-none} "${VARGS[@]}" $args \
         > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
       python - "$r" "$v" "$c" <<'PY'
 import json, sys
 d = json.loads([l for l in open("gpurun_out/ab.json") if l.startswith("{")][-1])
 kern = d.get("roofline", {}).get("kernel_ms", d.get("rank0_kernel_ms"))
 print(sys.argv[1], f"[{sys.argv[2]}]", f"[{sys.argv[3]}]", d.get("value"), d.get("ms_per_step"), kern, "cold", d.get("cold_ms"),
+      *(["distinct", d["value_distinct_samples"], d["distinct_samples"]["kernel_ms"]] if "distinct_samples" in d else []),
       flush=True)
 for r in d.get("runs", [])[1:]:  # (onrender: the other sizes / modes)
     print("   ", r["width"], r["mode"], r["mrays_per_s"], r["ms_per_frame"], "gpu", r.get("gpu_ms_per_frame"), flush=True)
