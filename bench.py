@@ -101,6 +101,11 @@ def parse():
     p.add_argument("--headline-only", action="store_true",
                    help="skip the extra legs after the timed steps (the brute-force roofline leg and the "
                         "distinct-samples leg): the PMC passes and kernel traces record the headline launches only")
+    p.add_argument("--distinct-base", type=int, default=-1,
+                   help="distinct leg: first frame of its first step (default spp x (warmup + 1))")
+    p.add_argument("--distinct-stride", type=int, default=-1,
+                   help="distinct leg: frames between its steps' first frames (default spp; 0 replays one range, "
+                        "the leg's control)")
     p.add_argument("--legs", default="distinct,brute",
                    help="extra legs after the timed steps (1 GPU, whole frame): 'distinct' (the same steps on "
                         "samples no launch has seen), 'brute' (the brute-force kernel's roofline), both, or 'none'")
@@ -513,24 +518,35 @@ def distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, o
     The last step is checked bit for bit against a FRESH device's cold render
     of the same frame range (its first launch: cull pass, split head, no
     learned order)."""
-    pc0 = S * (args.warmup + 1)
+    pc0 = S * (args.warmup + 1) if args.distinct_base < 0 else args.distinct_base
+    stride = S if args.distinct_stride < 0 else args.distinct_stride
     prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
     cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    ctr = torch.zeros(args.steps, dtype=torch.int64, device="cuda")
+    n = args.warmup + args.steps
+    ctr = torch.zeros(n, dtype=torch.int64, device="cuda")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def launch(i):
+        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
+                  rays_ptr=ctr[i].data_ptr(), prev_count=pc0 + stride * i, frames=S, max_bounce=B,
+                  simd=not args.scalar, band_rows=args.band_rows, accum_zero=True, stream=stream.cuda_stream)
+
+    # untimed warm-up launches on unseen frames too: the host work between the headline's timed
+    # steps and this leg idles the GPU, and its clock takes ~6 launches of C2 to ramp back
+    # (measured: 5.0, 4.7, 4.6, 4.4, 4.3, 4.2 ms, then steady, profiles/r06b_distinct_warmup.txt)
+    for i in range(args.warmup):
+        launch(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        dev.trace(cam, width=W, height=H, prev_ptr=prev.data_ptr(), cur_ptr=cur.data_ptr(),
-                  rays_ptr=ctr[i].data_ptr(), prev_count=pc0 + S * i, frames=S, max_bounce=B,
-                  simd=not args.scalar, band_rows=args.band_rows, accum_zero=True, stream=stream.cuda_stream)
+        launch(args.warmup + i)
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    counts = ctr.tolist()
+    counts = ctr[args.warmup:].tolist()
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    last_pc = pc0 + S * (args.steps - 1)
+    last_pc = pc0 + stride * (n - 1)
     fresh = rt.Device(gpu, options=opts)
     try:
         fresh.upload_scene(scene)
@@ -547,13 +563,16 @@ def distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, o
     same = (torch.equal(prev.view(torch.int32), cprev.view(torch.int32)) and torch.equal(cur, ccur)
             and counts[-1] == int(crays.item()))
     return {"value": round(sum(counts) / elapsed / 1e6, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "kernel_ms": round(kern_ms, 3), "segments_per_step": counts,
-            "frames": [pc0, last_pc + S], "verified_vs_fresh_device": bool(same),
+            "kernel_ms": round(kern_ms, 3), "kernel_ms_per_step": [round(a.elapsed_time(b), 3) for a, b in ev],
+            "segments_per_step": counts,
+            "frames_timed": [pc0 + stride * args.warmup, last_pc + S], "warmup_frames": [pc0, pc0 + stride * args.warmup],
+            "verified_vs_fresh_device": bool(same),
             "fresh_device_split_head_frames": cold_split,
-            "note": f"timed step i folds frames [{S}(w+1+i), {S}(w+2+i)) with RT_FLAG_ACCUM_ZERO: every launch "
-                    "traces samples (pixel seeds) no earlier launch traced, with the wave order and pixel "
-                    "permutation learned on other samples; the last step equals a fresh device's cold render of "
-                    "the same frames (v4, RGBA8, ray count)"}
+            "note": f"after w untimed launches (also on unseen frames), timed step i folds frames "
+                    f"[{S}(2w+1+i), {S}(2w+2+i)) with RT_FLAG_ACCUM_ZERO: every launch traces samples (pixel "
+                    "seeds) no earlier launch traced, with the wave order and pixel permutation learned on other "
+                    "samples; the last step equals a fresh device's cold render of the same frames (v4, RGBA8, "
+                    "ray count)"}
 
 
 def one_gpu_reference(rt, torch, dev, cam, args, W, H, S, B, stream, steps: int):
@@ -1037,6 +1056,8 @@ def main():
                                 "and the learned heaviest-first order"}
         line["roofline"] = roofline(args, info, kern_ms, rays_local, rows[0], W, N, workload, world, binary_hash,
                                     culled=opts.get("Cull", 0) != -1)
+        if per_launch_events:
+            line["kernel_ms_per_step"] = [round(a.elapsed_time(b), 3) for a, b in ev]
         if opts:
             line["config"]["device_options"] = opts
         if "brute" in legs:
