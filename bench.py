@@ -522,7 +522,8 @@ def distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, o
     stride = S if args.distinct_stride < 0 else args.distinct_stride
     prev = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
     cur = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    n = args.warmup + args.steps
+    warm = max(args.warmup, 6)
+    n = warm + args.steps
     ctr = torch.zeros(n, dtype=torch.int64, device="cuda")
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
@@ -531,20 +532,20 @@ def distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, o
                   rays_ptr=ctr[i].data_ptr(), prev_count=pc0 + stride * i, frames=S, max_bounce=B,
                   simd=not args.scalar, band_rows=args.band_rows, accum_zero=True, stream=stream.cuda_stream)
 
-    # untimed warm-up launches on unseen frames too: the host work between the headline's timed
+    # untimed warm-up launches (at least 6) on unseen frames too: the host work between the headline's timed
     # steps and this leg idles the GPU, and its clock takes ~6 launches of C2 to ramp back
     # (measured: 5.0, 4.7, 4.6, 4.4, 4.3, 4.2 ms, then steady, profiles/r06b_distinct_warmup.txt)
-    for i in range(args.warmup):
+    for i in range(warm):
         launch(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        launch(args.warmup + i)
+        launch(warm + i)
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    counts = ctr[args.warmup:].tolist()
+    counts = ctr[warm:].tolist()
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     last_pc = pc0 + stride * (n - 1)
     fresh = rt.Device(gpu, options=opts)
@@ -565,11 +566,11 @@ def distinct_leg(rt, torch, args, dev, scene, cam, W, H, S, N, B, gpu, stream, o
     return {"value": round(sum(counts) / elapsed / 1e6, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "kernel_ms": round(kern_ms, 3), "kernel_ms_per_step": [round(a.elapsed_time(b), 3) for a, b in ev],
             "segments_per_step": counts,
-            "frames_timed": [pc0 + stride * args.warmup, last_pc + S], "warmup_frames": [pc0, pc0 + stride * args.warmup],
+            "frames_timed": [pc0 + stride * warm, last_pc + S], "warmup_frames": [pc0, pc0 + stride * warm],
             "verified_vs_fresh_device": bool(same),
             "fresh_device_split_head_frames": cold_split,
-            "note": f"after w untimed launches (also on unseen frames), timed step i folds frames "
-                    f"[{S}(2w+1+i), {S}(2w+2+i)) with RT_FLAG_ACCUM_ZERO: every launch traces samples (pixel "
+            "note": f"after {warm} untimed launches (also on unseen frames), each timed step folds the next "
+                    f"{S} frames with RT_FLAG_ACCUM_ZERO: every launch traces samples (pixel "
                     "seeds) no earlier launch traced, with the wave order and pixel permutation learned on other "
                     "samples; the last step equals a fresh device's cold render of the same frames (v4, RGBA8, "
                     "ray count)"}

@@ -24,8 +24,11 @@ if [ "$part" = suite ]; then
   cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${W}_trace -o run --output-format csv -- python bench.py \
     > ${W}_trace.log 2>&1 || { tail -5 ${W}_trace.log; exit 1; }
-  f=$(find ${W}_trace -name "*kernel_trace.csv" | head -1)
-  python scripts/kernel_timeline.py "$f" --tail 5 > ${W}_timeline.txt || exit 1
+  # the headline's timed launches alone (--legs none): the last 5 dispatches of its kernel are the 5 timed steps
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${W}_trace_headline -o run --output-format csv -- python bench.py \
+    --legs none --no-cpu-baseline > ${W}_trace_headline.log 2>&1 || { tail -5 ${W}_trace_headline.log; exit 1; }
+  f=$(find ${W}_trace_headline -name "*kernel_trace.csv" | head -1)
+  python scripts/kernel_timeline.py "$f" --tail 5 --kernel "trace_kernel<true, 0, true" > ${W}_timeline.txt || exit 1
   for cfg in c3 rtw c2in; do
     timeout -k 10 300 python bench.py --config $cfg --steps 5 --warmup 3 --no-cpu-baseline --legs distinct \
       >> ${W}_configs.jsonl 2>> ${W}_configs.err || exit 1

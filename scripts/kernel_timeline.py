@@ -12,15 +12,19 @@ ap = argparse.ArgumentParser()
 ap.add_argument("csv")
 ap.add_argument("--tail", type=int, default=64, help="steady-state frames (trace-kernel dispatches) summarised")
 ap.add_argument("--show", type=int, default=24, help="kernels listed at the end")
+ap.add_argument("--kernel", default="trace_kernel",
+                help="name substring of the trace kernel whose dispatches mark the frames (e.g. 'trace_kernel<true, 0, "
+                     "true' for the culled headline kernel of a run that also has a brute-force leg)")
 a = ap.parse_args()
 
 rows = list(csv.DictReader(open(a.csv)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-trace_idx = [i for i, r in enumerate(rows) if "trace_kernel" in r["Kernel_Name"]]
+trace_idx = [i for i, r in enumerate(rows) if a.kernel in r["Kernel_Name"]]
+rows = rows[:trace_idx[-1] + 1]  # up to the last dispatch of that kernel
 first = trace_idx[-a.tail] if len(trace_idx) >= a.tail else trace_idx[0]
 steady = rows[first:]
 t0, t1 = int(steady[0]["Start_Timestamp"]), int(steady[-1]["End_Timestamp"])
-frames = sum(1 for r in steady if "trace_kernel" in r["Kernel_Name"])
+frames = sum(1 for r in steady if a.kernel in r["Kernel_Name"])
 dur = collections.defaultdict(list)
 busy = 0
 prev_end = None
