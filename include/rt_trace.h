@@ -481,8 +481,9 @@ int rt_debug_stats(rt_device *dev, uint64_t out[32], int reset);
  * Returns the number of waves copied (0 when disabled), < 0 on error. */
 int64_t rt_debug_wave_times(rt_device *dev, uint64_t *out, uint64_t max_waves);
 
-/* The cull pass's primary group masks of the last culled launch geometry:
- * word ((tile * 4 + wave) * n_words + w), n_words = ceil(groups / 64).
+/* The cull pass's primary masks of the last culled launch geometry, one bit
+ * per sphere pair (bit p: spheres 2p and 2p + 1, i.e. half p & 1 of group
+ * p >> 1): word ((tile * 4 + wave) * n_words + w), n_words = ceil(2 groups / 64).
  * Returns the number of words copied (0 when no cull pass ran), < 0 on error.
  * Test hook: tests/test_gpu_parity.py checks them against a CPU restatement. */
 int64_t rt_debug_masks(rt_device *dev, uint64_t *out, uint64_t max_words);

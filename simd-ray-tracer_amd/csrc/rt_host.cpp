@@ -1100,7 +1100,7 @@ static int apply_reserve(rt_device *d) {
     const uint32_t n_tiles = d->reserve_tiles;
     uint32_t n_words = 1;
     if (d->scene_set)
-        for (int rs = 0; rs < 2; ++rs) n_words = std::max(n_words, (d->n_groups[rs] + 63u) / 64u);
+        for (int rs = 0; rs < 2; ++rs) n_words = std::max(n_words, rtk_mask_words(d->n_groups[rs]));
     if (const int rc = ensure_tile_buffers(d, n_tiles, nullptr, true)) return rc;
     if (d->pixel_sort_env)
         if (const int rc = ensure_pixel_sort(d, n_tiles, d->reserve_pixels, nullptr, true))
@@ -1270,7 +1270,7 @@ extern "C" int rt_trace(rt_device *d, const rt_camera_info *cam, const rt_trace_
     // its own workgroup, so each is placed by its own cost), block tiles otherwise
     a.unit_waves = a.solo && d->wave_order_env ? 1u : 0u;
     const uint32_t n_units = a.unit_waves ? 4u * n_tiles : n_tiles;
-    const uint32_t n_words = (a.n_groups + 63u) / 64u;
+    const uint32_t n_words = rtk_mask_words(a.n_groups);
     const bool cull = d->cull != 0;
     const bool empty_capable = cull && !d->use_sky && desc->MaxBounce != 0;
     const bool sched = d->tile_sched != 0;

@@ -143,6 +143,10 @@ constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many
 // weight table), so the table is then read from HBM through the caches.
 // The 2 KB weight table of the first 256 frames goes the same way (the
 // weights are then two divisions per sample): C5 fits 7 blocks per CU.
+// The cull pass's primary masks hold one bit per sphere PAIR (spheres 2p, 2p + 1: half p & 1 of group
+// p >> 1), so a primary round tests only the pairs its tile's cone may reach -- half of the group-level
+// masks' pair tests at C2 (1.17 of 2.33 pairs per live 4x4 tile); words per wave tile:
+static inline __host__ __device__ uint32_t rtk_mask_words(uint32_t n_groups) { return (2u * n_groups + 63u) / 64u; }
 static inline bool rtk_lut_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
 static inline bool rtk_fold_in_lds(uint32_t n_groups) { return n_groups <= 32u; }
 static inline size_t rtk_scene_lds_bytes(uint32_t n_groups) {
@@ -156,7 +160,7 @@ static inline size_t rtk_lds_bytes(const TraceArgs *a) {
 // the two tables): 265 groups = 1,060 spheres.  Larger scenes stay in HBM
 // (scene_in_lds = 0): the sphere loop reads groups through the scalar cache as
 // always, and the per-lane gathers go through L1/L2.  Up to kMaxGroups groups
-// (the primary cull masks are kMaxGroups / 64 words per wave tile).
+// (the primary cull masks are rtk_mask_words(kMaxGroups) = 128 words per wave tile).
 static const uint32_t kMaxLdsGroups = (65536u - 8192u - 2048u) / (16u * kGroupF4 + 64u * kSphereF4);  // 164 groups
 static const uint32_t kMaxGroups = 4096u;                                                    // 16,384 spheres
 

@@ -883,33 +883,38 @@ __device__ __forceinline__ f2 pair_dist_c(const RayPk &r, f2 cx, f2 cy, f2 cz, f
     return d;
 }
 
-// test_group for a primary round: group g's camera-relative rows (TraceArgs.prim).
+// One sphere pair of a primary round (spheres L0, L0 + 1 of group g, camera-relative rows from
+// TraceArgs.prim): test_group's two halves as separate pair tests.
+template <bool SIMD, int L0>
+__device__ __forceinline__ void test_half_prim(const TraceArgs &a, uint32_t g, const RayPk &p, Hit &h, f2 cx, f2 cy,
+                                               f2 cz, float r2a, float r2b) {
+    f2 T;
+    const f2 d = pair_dist_c(p, cx, cy, cz, T);
+    bool ha, hb;
+    if (SIMD) {  // HitMask = d < r^2 (main.cpp:409)
+        ha = d.x < r2a;
+        hb = d.y < r2b;
+    } else {  // !(d > r^2) over the Count real spheres only (main.cpp:547,557)
+        const uint32_t s0 = 4u * g + (uint32_t)L0;
+        ha = s0 < a.n_spheres && !(d.x > r2a);
+        hb = s0 + 1u < a.n_spheres && !(d.y > r2b);
+    }
+    if (ha | hb) {
+        if (ha) candidate<SIMD, L0>(h, g, T.x, d.x, r2a, a.fast_sqrt != 0u);
+        if (hb) candidate<SIMD, L0 + 1>(h, g, T.y, d.y, r2b, a.fast_sqrt != 0u);
+    }
+}
+
+// Pair pr of a primary round's pair mask (half pr & 1 of group pr >> 1); the mask's pairs come in
+// ascending order, the reference's sphere order, so the per-class minima and tie rules are those of
+// the full group loop.
 template <bool SIMD>
-__device__ __forceinline__ void test_group_prim(const TraceArgs &a, cv4f_t *prim, uint32_t g, const RayPk &p, Hit &h) {
+__device__ __forceinline__ void test_pair_prim(const TraceArgs &a, cv4f_t *prim, uint32_t pr, const RayPk &p, Hit &h) {
+    const uint32_t g = pr >> 1;
     cv4f_t *pg = prim + kPrimF4 * g;
     const v4f_t cx = pg[0], cy = pg[1], cz = pg[2], r2 = pg[3];
-    f2 T01, T23;
-    const f2 d01 = pair_dist_c(p, f2{cx.x, cx.y}, f2{cy.x, cy.y}, f2{cz.x, cz.y}, T01);
-    const f2 d23 = pair_dist_c(p, f2{cx.z, cx.w}, f2{cy.z, cy.w}, f2{cz.z, cz.w}, T23);
-    bool h0, h1, h2, h3;
-    if (SIMD) {  // HitMask = d < r^2 (main.cpp:409)
-        h0 = d01.x < r2.x;
-        h1 = d01.y < r2.y;
-        h2 = d23.x < r2.z;
-        h3 = d23.y < r2.w;
-    } else {  // !(d > r^2) over the Count real spheres only (main.cpp:547,557)
-        const uint32_t s0 = 4u * g;
-        h0 = s0 + 0u < a.n_spheres && !(d01.x > r2.x);
-        h1 = s0 + 1u < a.n_spheres && !(d01.y > r2.y);
-        h2 = s0 + 2u < a.n_spheres && !(d23.x > r2.z);
-        h3 = s0 + 3u < a.n_spheres && !(d23.y > r2.w);
-    }
-    if (h0 | h1 | h2 | h3) {
-        if (h0) candidate<SIMD, 0>(h, g, T01.x, d01.x, r2.x, a.fast_sqrt != 0u);
-        if (h1) candidate<SIMD, 1>(h, g, T01.y, d01.y, r2.y, a.fast_sqrt != 0u);
-        if (h2) candidate<SIMD, 2>(h, g, T23.x, d23.x, r2.z, a.fast_sqrt != 0u);
-        if (h3) candidate<SIMD, 3>(h, g, T23.y, d23.y, r2.w, a.fast_sqrt != 0u);
-    }
+    if (pr & 1u) test_half_prim<SIMD, 2>(a, g, p, h, f2{cx.z, cx.w}, f2{cy.z, cy.w}, f2{cz.z, cz.w}, r2.z, r2.w);
+    else test_half_prim<SIMD, 0>(a, g, p, h, f2{cx.x, cx.y}, f2{cy.x, cy.y}, f2{cz.x, cz.y}, r2.x, r2.y);
 }
 
 // Conservative per-wave culling for primary rays.  All primary rays of a
@@ -990,11 +995,11 @@ constexpr bool kStats = false;
 #endif
 
 constexpr int kWavesPerBlock = 4;
-// primary group mask words per wave tile: the LDS-image kernels keep this
+// primary pair mask words per wave tile (rtk_mask_words): the LDS-image kernels keep this
 // small (it is static LDS, and C2's blocks fill the CU's 160 KB 7 times)
 template <bool GS>
 struct MaskWords {
-    static constexpr int N = GS ? (int)((kMaxGroups + 63u) / 64u) : (int)((kMaxLdsGroups + 63u) / 64u);
+    static constexpr int N = GS ? (int)((2u * kMaxGroups + 63u) / 64u) : (int)((2u * kMaxLdsGroups + 63u) / 64u);
 };
 constexpr uint32_t kFoldTable = 256;
 // Per-pixel out-of-order sample slots (LDS ring): at least P (every sample
@@ -1203,15 +1208,16 @@ void trace_kernel(TraceArgs a) {
     constexpr bool kCursorPerLane = LP > 1;
     float4 *ring = s_ring + sw * kRing * kRingStride + pl;
 
-    const uint32_t n_words = (a.n_groups + 63u) / 64u;
-    // the wave tile's primary group mask, from the cull pass (rtk_launch_cull)
+    const uint32_t n_words = rtk_mask_words(a.n_groups);
+    // the wave tile's primary pair mask, from the cull pass (rtk_launch_cull)
     // (a permuted wave's pixels come from all four quadrants: the union of their masks)
-    if (CULL && lane < n_words) {
-        uint64_t m = a.masks[((size_t)tile * 4u + wave) * n_words + lane];
-        if (permuted)
-            for (uint32_t q = 0; q < 4u; ++q) m |= a.masks[((size_t)tile * 4u + q) * n_words + lane];
-        s_maskw[lane] = m;
-    }
+    if (CULL)
+        for (uint32_t wd = lane; wd < n_words; wd += 64u) {
+            uint64_t m = a.masks[((size_t)tile * 4u + wave) * n_words + wd];
+            if (permuted)
+                for (uint32_t q = 0; q < 4u; ++q) m |= a.masks[((size_t)tile * 4u + q) * n_words + wd];
+            s_maskw[wd] = m;
+        }
     const uint64_t st_c1 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
     __syncthreads();
     const uint64_t st_c2 = kStats && a.stats ? __builtin_amdgcn_s_memtime() : 0;
@@ -1519,10 +1525,10 @@ void trace_kernel(TraceArgs a) {
                                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_maskw[w] >> 32));
                             uint64_t m = (uint64_t)lo | ((uint64_t)hi << 32);
                             if (kStats && a.stats) st_groups += __builtin_popcountll(m);
-                            while (m) {
-                                const uint32_t g = w * 64u + (uint32_t)__builtin_ctzll(m);
+                            while (m) {  // the tile's sphere pairs, in the reference's order
+                                const uint32_t pr = w * 64u + (uint32_t)__builtin_ctzll(m);
                                 m &= m - 1;
-                                test_group_prim<SIMD>(a, prim, g, ray, h);
+                                test_pair_prim<SIMD>(a, prim, pr, ray, h);
                             }
                         }
                     } else {
@@ -1726,27 +1732,30 @@ void trace_kernel(TraceArgs a) {
     }
 }
 
-// Primary-ray culling of one wave tile (TW x TH pixels at x0, ly0): bit g of
-// the mask is set when some sphere of group g may pass some primary ray's
-// exact test (cone_may_hit).  One sphere per lane, 64 per ballot, folded
-// into one bit per group; word w covers groups 64w .. 64w+63.
+// Primary-ray culling of one wave tile (TW x TH pixels at x0, ly0): bit p of
+// the mask is set when some sphere of pair p (sphere slots 2p, 2p + 1: half
+// p & 1 of group p >> 1) may pass some primary ray's exact test
+// (cone_may_hit).  One sphere per lane, 64 per ballot, folded into one bit
+// per pair; word w covers pairs 64w .. 64w+63 (spheres 128w .. 128w+127).
 template <int P>
 __device__ __forceinline__ uint64_t wave_tile_mask(const TraceArgs &a, const Cone &c, uint32_t w, uint32_t lane) {
     const float *gf = reinterpret_cast<const float *>(a.groups);
     uint64_t gm = 0;
-    for (uint32_t q = 0; q < 4u && (w * 64u + q * 16u) < a.n_groups; ++q) {
-        const uint32_t sph = (w * 64u + q * 16u) * 4u + lane;  // sphere slot 4*g + l
+    for (uint32_t q = 0; q < 2u && w * 128u + q * 64u < 4u * a.n_groups; ++q) {
+        const uint32_t sph = w * 128u + q * 64u + lane;  // sphere slot 4*g + l
         bool cand = false;
         if (sph < 4u * a.n_groups) {
             const float *row = gf + (size_t)(sph >> 2) * (4u * kGroupF4) + (sph & 3u);
             cand = cone_may_hit(a, c, row[4u * kRowX], row[4u * kRowY], row[4u * kRowZ], row[4u * kRowR2]);
         }
         uint64_t m = __ballot(cand);
-        m |= (m >> 1) | (m >> 2) | (m >> 3);  // bit 4i: some sphere of group 16q+i
-        uint64_t bits = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 16u; ++i) bits |= ((m >> (4u * i)) & 1u) << i;
-        gm |= bits << (16u * q);
+        m = (m | (m >> 1)) & 0x5555555555555555ull;  // bit 2i: some sphere of pair 32q + i
+        m = (m | (m >> 1)) & 0x3333333333333333ull;  // compress the even bits into bits 0..31
+        m = (m | (m >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        m = (m | (m >> 4)) & 0x00FF00FF00FF00FFull;
+        m = (m | (m >> 8)) & 0x0000FFFF0000FFFFull;
+        m = (m | (m >> 16)) & 0x00000000FFFFFFFFull;
+        gm |= m << (32u * q);
     }
     return gm;
 }
@@ -1782,7 +1791,7 @@ __global__ __launch_bounds__(256) void cull_kernel(TraceArgs a, uint32_t *live, 
     const uint32_t y0 = ((ly0 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly0 % a.band_rows;
     const uint32_t y1 = ((ly1 / a.band_rows) * a.band_count + a.band_index) * a.band_rows + ly1 % a.band_rows;
     const Cone c = tile_cone(a, (double)x0 - 0.501, (double)x1 + 0.501, (double)y0 - 0.501, (double)y1 + 0.501);
-    const uint32_t n_words = (a.n_groups + 63u) / 64u;
+    const uint32_t n_words = rtk_mask_words(a.n_groups);
     bool any = false;
     for (uint32_t w = 0; w < n_words; ++w) {
         const uint64_t gm = wave_tile_mask<P>(a, c, w, lane);
@@ -1895,7 +1904,7 @@ __global__ __launch_bounds__(64) void pixel_sort_kernel(TraceArgs a, uint8_t *pe
     uint8_t *pp = perm + (size_t)tile * 64u;
     // a quadrant without candidate groups folds without tracing: keep such blocks as they are
     if (a.masks) {
-        const uint32_t n_words = (a.n_groups + 63u) / 64u;
+        const uint32_t n_words = rtk_mask_words(a.n_groups);
         bool live = false;
         for (uint32_t w = 0; lane < 4u && w < n_words; ++w) live = live || a.masks[((size_t)tile * 4u + lane) * n_words + w] != 0;
         if (__builtin_popcountll(__ballot(lane < 4u && live)) != 4) {
@@ -2279,7 +2288,7 @@ template <int P>
 static void launch_p(const TraceArgs *a, int simd, int src, int cull, uint32_t n_blocks, hipStream_t stream) {
     const dim3 block(256), grid(n_blocks);
     const size_t lds = rtk_lds_bytes(a);
-    const size_t solo_lds = 8u * ((a->n_groups + 63u) / 64u);  // one-wave kernels: the cull mask words
+    const size_t solo_lds = 8u * rtk_mask_words(a->n_groups);  // one-wave kernels: the cull mask words
 #define RTK_LAUNCH(S, R, C, G) hipLaunchKernelGGL((rtk::trace_kernel<S, R, C, P, G>), grid, block, lds, stream, *a)
 #define RTK_LAUNCH_SOLO(S, C, K) \
     hipLaunchKernelGGL((rtk::trace_kernel<S, kSrcSmem, C, P, true, true, K>), dim3(4u * n_blocks), dim3(64), solo_lds, \

@@ -1,8 +1,9 @@
-"""CPU restatement (numpy, f64) of the cull pass's primary group masks
+"""CPU restatement (numpy, f64) of the cull pass's primary masks
 (rt_kernel.hip tile_cone / cone_may_hit / wave_tile_mask), SIMD rule set,
-one band: one u64 word per 64 groups per wave tile, word
-((tile * 4 + wave) * n_words + w).  Test helper (test_gpu_parity.py,
-test_cull_bound.py, scripts/diag)."""
+one band: one bit per sphere pair (bit p: sphere slots 2p, 2p + 1), one u64
+word per 64 pairs per wave tile, word ((tile * 4 + wave) * n_words + w),
+n_words = ceil(2 groups / 64) (rt_kernel.h rtk_mask_words).  Test helper
+(test_gpu_parity.py, test_cull_bound.py, test_random_scene_bounds.py)."""
 import numpy as np
 
 SHAPE = {1: (8, 8), 2: (8, 4), 4: (4, 4), 8: (4, 2), 16: (2, 2)}  # wave tile TW x TH per lanes-per-pixel
@@ -33,7 +34,7 @@ def np_masks(rt, scene, cam, W, H, P):
     cp, camx, camy, fc = _v3(cam.CameraPosition), _v3(cam.CameraX), _v3(cam.CameraY), _v3(cam.FilmCenter)
     fw, fh = float(np.float32(cam.FilmW)), float(np.float32(cam.FilmH))
     TW, TH = SHAPE[P]
-    nw = (ng + 63) // 64
+    nw = (2 * ng + 63) // 64
     tiles = list(wave_tiles(W, H, P))
     out = np.zeros(len(tiles) * nw, np.uint64)
     q = c - cp
@@ -60,7 +61,7 @@ def np_masks(rt, scene, cam, W, H, P):
             cos_lim = cos_t * cb - sin_t * sb
             cos_phi = np.abs(q @ ax) / np.sqrt(c2)
             cand = (r2 >= 0) & ((rr >= c2) | (cos_t <= 0) | (cos_phi >= cos_lim - 1e-12))
-        gm = cand.reshape(-1, 4).any(1)
+        gm = cand.reshape(-1, 2).any(1)  # per sphere pair
         for wd in range(nw):
             bits = 0
             for gi in np.flatnonzero(gm[64 * wd:64 * wd + 64]):
@@ -69,9 +70,9 @@ def np_masks(rt, scene, cam, W, H, P):
     return out
 
 
-def sampled_hit_groups(rt, scene, cam, W, H, x, y, n_jitter=9):
-    """Groups whose spheres some f64 primary ray of pixel (x, y) passes within
-    r of (a jitter grid over the pixel's +-0.5 px)."""
+def sampled_hit_pairs(rt, scene, cam, W, H, x, y, n_jitter=9):
+    """Sphere pairs (slots 2p, 2p + 1) some f64 primary ray of pixel (x, y)
+    passes within r of (a jitter grid over the pixel's +-0.5 px)."""
     c, r2, _ = scene_spheres(rt, scene)
     cp, camx, camy, fc = _v3(cam.CameraPosition), _v3(cam.CameraX), _v3(cam.CameraY), _v3(cam.FilmCenter)
     hits = set()
@@ -84,5 +85,5 @@ def sampled_hit_groups(rt, scene, cam, W, H, x, y, n_jitter=9):
             d /= np.linalg.norm(d)
             T = C @ d
             dist = (C * C).sum(1) - T * T
-            hits.update(int(i) // 4 for i in np.flatnonzero((dist < r2) & (r2 > 0)))
+            hits.update(int(i) // 2 for i in np.flatnonzero((dist < r2) & (r2 > 0)))
     return hits

@@ -609,9 +609,9 @@ def test_stream_switch_keeps_every_bit(rt, orc, torch_cuda):
 @pytest.mark.parametrize("idx,n,W,H,P", [(1, 64, 96, 64, 4), (1, 128, 16, 16, 1), (1, 200, 40, 32, 2),
                                          (1, 256, 64, 48, 8), (0, None, 48, 32, 16)])
 def test_cull_masks_equal_cpu_restatement(rt, torch_cuda, idx, n, W, H, P):
-    """The cull pass's primary group masks (rt_debug_masks) equal the numpy f64
-    restatement (tests/cull_ref.py) word for word; tests/test_cull_bound.py
-    checks that restatement keeps every group a pixel's rays can reach."""
+    """The cull pass's primary sphere-pair masks (rt_debug_masks) equal the numpy
+    f64 restatement (tests/cull_ref.py) word for word; tests/test_cull_bound.py
+    checks that restatement keeps every pair a pixel's rays can reach."""
     from cull_ref import np_masks
     s = rt.scene_builtin(idx)
     if n:
@@ -739,12 +739,13 @@ def test_upload_waits_for_traces_in_flight(rt, orc, torch_cuda):
         assert_same(p, c, n, *r)
 
 
-@pytest.mark.parametrize("n_spheres", [1061, 2000, 4099])
+@pytest.mark.parametrize("n_spheres", [1061, 2000, 4099, 9001])
 def test_scene_beyond_the_lds_image(rt, orc, torch_cuda, gdev, n_spheres):
     """Scenes above 656 spheres (164 groups) stay in HBM even for the four-wave
     kernels (the one-wave default keeps every scene there): the sphere loop
     reads groups through the scalar cache and the winner / material / r^2
-    gathers go through the caches.  RTWeekend's 482 spheres plus small spheres
+    gathers go through the caches.  9,001 spheres (2,251 groups) take 71 words of
+    the primary pair mask per wave tile, more than the 64 lanes that load them.  RTWeekend's 482 spheres plus small spheres
     scattered over its ground, both rule sets, bit-exact against the oracle."""
     base = rt.scene_builtin(2)
     sp0, _, _ = rt.scene_arrays(base)

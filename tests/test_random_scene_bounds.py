@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import random_scenes
-from cull_ref import SHAPE, np_masks, sampled_hit_groups, scene_spheres, wave_tiles
+from cull_ref import SHAPE, np_masks, sampled_hit_pairs, scene_spheres, wave_tiles
 from test_prefilter_bound import check_clusters, check_prefilter
 
 SEEDS = list(range(40))
@@ -36,14 +36,14 @@ def test_random_scene_bounds(rt, orc, seed):
         masks = np_masks(rt, s, cam, W, H, P)
         tiles = list(wave_tiles(W, H, P))
         nw = len(masks) // len(tiles)
-        ng = scene_spheres(rt, s)[2]
+        n_pairs = 2 * scene_spheres(rt, s)[2]
         for t, w, x0, y0 in tiles:
             words = [int(masks[(t * 4 + w) * nw + k]) for k in range(nw)]
-            _seen["cull_culls"] += ng - sum(bin(v).count("1") for v in words) > 0
+            _seen["cull_culls"] += n_pairs - sum(bin(v).count("1") for v in words) > 0
             for y in range(y0, min(y0 + TH, H), 2):
                 for x in range(x0, min(x0 + TW, W), 2):
-                    for gi in sampled_hit_groups(rt, s, cam, W, H, x, y, n_jitter=3):
-                        assert (words[gi // 64] >> (gi % 64)) & 1, f"{kind}: pixel ({x},{y}) reaches group {gi}"
+                    for pi in sampled_hit_pairs(rt, s, cam, W, H, x, y, n_jitter=3):
+                        assert (words[pi // 64] >> (pi % 64)) & 1, f"{kind}: pixel ({x},{y}) reaches pair {pi}"
 
 
 def test_random_scenes_exercise_every_skip(rt, orc):
@@ -63,7 +63,7 @@ def test_random_scenes_exercise_every_skip(rt, orc):
             seen["behind_skips"] += bh > 0
         cam = rt.camera_setup(scene, 24, 16)
         masks = np_masks(rt, scene, cam, 24, 16, 4)
-        ng = scene_spheres(rt, scene)[2]
-        nw = (ng + 63) // 64
-        seen["cull_culls"] += sum(bin(int(v)).count("1") for v in masks) < (len(masks) // nw) * ng
+        n_pairs = 2 * scene_spheres(rt, scene)[2]
+        nw = (n_pairs + 63) // 64
+        seen["cull_culls"] += sum(bin(int(v)).count("1") for v in masks) < (len(masks) // nw) * n_pairs
     assert all(v > 0 for v in seen.values()), seen
