@@ -15,7 +15,10 @@ identical.  Writes profiles/<tag>_cpu_calibration.json; bench.py reports its
 ratio as cpu_baseline.same_host_ratio_to_reference.  Needs /root/reference
 (this container), so the GPU box only reads the committed record.
 
-    python scripts/cpu_calibrate.py r05 [--rounds 9] [--threads 8]
+    python scripts/cpu_calibrate.py r06 [--rounds 9] [--threads 8] [--warmup 3]
+
+Round 6: each thread count starts with --warmup discarded alternating rounds (the round-5 record's first 8-worker
+rounds ran at the single-thread rate on both sides: the pool's threads had not spread over the cores yet).
 """
 import argparse
 import ctypes
@@ -47,6 +50,7 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--warmup", type=int, default=3, help="discarded alternating rounds before each thread count")
     a = ap.parse_args()
     P = ctypes.CDLL(str(ROOT / "oracle" / "_ref" / "librefpix.so"))
     v, u32 = ctypes.c_void_p, ctypes.c_uint32
@@ -87,13 +91,16 @@ def main():
            "runs": {}}
     for threads in (1, a.threads):
         rr, pr = [], []
+        for i in range(a.warmup):
+            ref(threads)
+            port(threads)
         for i in range(a.rounds):  # alternate, so drifting host load hits both sides alike
             r, rc, rrays = ref(threads)
             p, pc, prays = port(threads)
             assert rrays == prays and np.array_equal(rc, pc), "the port's frame differs from the reference's"
             rr.append(r)
             pr.append(p)
-        run = {"threads": threads, "rounds": a.rounds, "rays": rrays,
+        run = {"threads": threads, "rounds": a.rounds, "warmup_rounds_discarded": a.warmup, "rays": rrays,
                "reference_mrays_per_s": {"median": round(statistics.median(rr), 3), "best": round(max(rr), 3),
                                          "all": [round(x, 3) for x in rr]},
                "port_mrays_per_s": {"median": round(statistics.median(pr), 3), "best": round(max(pr), 3),
