@@ -222,13 +222,36 @@ def combine_verified(vs_one_gpu, vs_golden):
     return None if not checks else all(checks)
 
 
+def reference_lib():
+    """oracle/_ref/librefpix.so: the reference's own main.cpp:7-640 (RenderTile, with SURVEY 8c's pixel-seed and
+    bounce-count patches) compiled from /root/reference in the build container by `make -C oracle ref` with its own
+    codegen flags; the built .so travels with the tree (git-ignored, not gpurun-ignored), so the GPU box can time
+    the reference itself.  None when it was not built."""
+    import ctypes
+    path = ROOT / "oracle" / "_ref" / "librefpix.so"
+    if not path.exists():
+        return None
+    L = ctypes.CDLL(str(path))
+    v, u32 = ctypes.c_void_p, ctypes.c_uint32
+    L.ref_set_patch.restype = None
+    L.ref_set_patch.argtypes = [u32, ctypes.c_int]
+    L.ref_render_threads.restype = None
+    L.ref_render_threads.argtypes = [v, u32, v, u32, v, u32, u32, v, u32, u32, u32, u32, ctypes.c_int, u32, v, v, v]
+    return L
+
+
 def cpu_baseline(args, n_rays_gpu_step: int):
-    """The oracle (C restatement of RenderTile, lane-4 SSE, pthread 32x32 tile
-    queue, compiled like the reference: clang -O3 -mavx2 -mfma) on this host's
-    cores, on a bounded sample of the same workload: the full 1920x1080 frame,
-    64 spheres, 8 bounces, k spp, k chosen from a 1-spp calibration so the
-    sample takes ~--cpu-seconds.  Its speed relative to the reference's own
-    compiled RenderTile is the committed same-host calibration record."""
+    """The CPU baseline on this host's cores, on a bounded sample of the same workload: the full frame at k spp, k
+    chosen from a 1-spp probe so the alternating rounds take ~--cpu-seconds in all.
+
+    kind "reference": the reference's own compiled RenderTile (oracle/_ref/librefpix.so, its tiles pulled by
+    `threads` workers from one counter as its work queue deals them, wasm/wasm.cpp:624-694), pixel seeds, the
+    workload's bounce count.  The port (oracle/rt_oracle.c, the C restatement) is timed on the same sample beside it,
+    so the line carries their live same-host ratio, also on the single-thread SURVEY 8d probe.  (The reference's
+    NormalizeFast is the host's rsqrtss: on a non-Intel host its frames differ from the Intel-table port's in a few
+    bits, `frames_identical`; the speed comparison does not depend on that.)  Without the reference build, kind
+    "port" with the committed same-host calibration record."""
+    import numpy as np
     from oracle import oracle as orc
     threads = orc.cpu_threads()
     env_cap = os.environ.get("OMP_NUM_THREADS")
@@ -237,44 +260,94 @@ def cpu_baseline(args, n_rays_gpu_step: int):
     o = orc.scene_builtin(args.scene)
     if args.spheres < len(o.spheres):
         o = o.prefix(args.spheres)
-    W, H = args.width, args.height
+    W, H, B = args.width, args.height, args.bounces
     cam = orc.camera(o, W, H, distance=args.distance)
-    t = time.perf_counter()
-    _, _, rays1 = orc.render(o, cam, W, H, frames=1, max_bounce=args.bounces, threads=threads, simd=not args.scalar)
-    dt1 = time.perf_counter() - t
-    k = max(1, min(args.spp, int(args.cpu_seconds / max(dt1, 1e-3))))
-    t = time.perf_counter()
-    _, _, rays = orc.render(o, cam, W, H, frames=k, max_bounce=args.bounces, threads=threads, simd=not args.scalar)
-    dt = time.perf_counter() - t
-    # the port counts as the reference's speed only if its single-thread
-    # rate is within +-10 % of the verbatim reference's on the probe workload
-    # (480x270, 8 spp, N = 64, 8 bounces, one thread: ~11-12.5 Mrays/s on the survey host)
-    p = orc.scene_builtin(1).prefix(64)
-    pc = orc.camera(p, 480, 270)
-    t = time.perf_counter()
-    _, _, prays = orc.render(p, pc, 480, 270, frames=8, max_bounce=8, threads=1)
-    pdt = time.perf_counter() - t
-    single = prays / pdt / 1e6
-    calib = cpu_calibration()
-    out = {"value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "cores": threads, "kind": "port",
-           "sample": f"{W}x{H}, {k} spp (of {args.spp}), {args.spheres} spheres, {args.bounces} bounces, "
-                     f"{rays} rays in {dt:.2f} s on {threads} threads (oracle/rt_oracle.c, lane-4 SSE "
-                     f"RenderTile restatement, pixel seeds)",
+    ref = reference_lib()
+
+    def port(scene, c, w, h, frames, thr, bounces):
+        t = time.perf_counter()
+        _, cur, rays = orc.render(scene, c, w, h, frames=frames, max_bounce=bounces, threads=thr,
+                                  simd=not args.scalar)
+        return rays, time.perf_counter() - t, cur
+
+    def reference(scene, c, w, h, frames, thr, bounces):
+        prev = np.zeros((w * h, 4), np.float32)
+        cur = np.zeros(w * h, np.uint32)
+        rays = np.zeros(1, np.uint64)
+        ref.ref_set_patch(bounces, 1)
+        t = time.perf_counter()
+        ref.ref_render_threads(scene.spheres.ctypes.data, len(scene.spheres), scene.groups.ctypes.data,
+                               len(scene.groups), scene.materials.ctypes.data, len(scene.materials), int(scene.use_sky),
+                               c.ctypes.data, w, h, 0, frames, int(not args.scalar), thr, prev.ctypes.data,
+                               cur.ctypes.data, rays.ctypes.data)
+        dt = time.perf_counter() - t
+        ref.ref_set_patch(5, 0)
+        return int(rays[0]), dt, cur
+
+    timed = reference if ref is not None else port
+    # warm-up (the host's scheduler spreads a fresh pool over the cores only after a while: short first runs
+    # measured single-core rates, profiles/r05_cpu_calibration.json) and the 1-spp probe that sizes k
+    timed(o, cam, W, H, 1, threads, B)
+    if ref is not None:
+        port(o, cam, W, H, 1, threads, B)
+    _, dt1, _ = timed(o, cam, W, H, 1, threads, B)
+    rounds = 3 if ref is not None else 1
+    k = max(1, min(args.spp, int(args.cpu_seconds / (2 * rounds if ref is not None else 1) / max(dt1, 1e-3))))
+    # SURVEY §8d's single-thread probe (480x270, 8 spp, N = 64, 8 bounces, one thread)
+    pr = orc.scene_builtin(1).prefix(64)
+    pcam = orc.camera(pr, 480, 270)
+    runs, pruns, probes, pprobes = [], [], [], []
+    for _ in range(rounds):  # alternating rounds (reference, port), medians reported
+        runs.append(timed(o, cam, W, H, k, threads, B))
+        probes.append(timed(pr, pcam, 480, 270, 8, 1, 8))
+        if ref is not None:
+            pruns.append(port(o, cam, W, H, k, threads, B))
+            pprobes.append(port(pr, pcam, 480, 270, 8, 1, 8))
+
+    def median(rs):  # (rays, seconds, frame) of the median-rate run
+        return sorted(rs, key=lambda r: r[0] / r[1])[len(rs) // 2]
+    rays, dt, cur = median(runs)
+    prays, pdt, _ = median(probes)
+    out = {"value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "cores": threads,
+           "kind": "reference" if ref is not None else "port",
+           "sample": f"{W}x{H}, {k} spp (of {args.spp}), {args.spheres} spheres, {B} bounces, {rays} rays in "
+                     f"{dt:.2f} s on {threads} threads (" +
+                     ("the reference's own RenderTile, main.cpp:7-640 compiled with its codegen flags "
+                      "(oracle/_ref/librefpix.so), pixel seeds, its tiles pulled from one counter"
+                      if ref is not None else "oracle/rt_oracle.c, lane-4 SSE RenderTile restatement, pixel seeds") +
+                     ")",
            "cpu": cpu_model(), "nproc": os.cpu_count(),
-           "single_thread": {"value": round(single, 2), "unit": "Mrays/s",
+           "single_thread": {"value": round(prays / pdt / 1e6, 2), "unit": "Mrays/s",
                              "sample": f"480x270, 8 spp, 64 spheres, 8 bounces, 1 thread, {prays} rays in "
                                        f"{pdt:.2f} s (SURVEY 8d calibration workload)"}}
+    if ref is not None:
+        # the port on the same sample and cores, alternating with the reference: the live same-host ratio
+        p_rays, p_dt, p_cur = median(pruns)
+        pp_rays, pp_dt, _ = median(pprobes)
+        out["rounds"] = {"reference": [round(r[0] / r[1] / 1e6, 2) for r in runs],
+                         "port": [round(r[0] / r[1] / 1e6, 2) for r in pruns],
+                         "note": "alternating rounds after a warm-up; value and port.value are the medians"}
+        out["port"] = {"value": round(p_rays / p_dt / 1e6, 2), "unit": "Mrays/s", "cores": threads,
+                       "single_thread": round(pp_rays / pp_dt / 1e6, 2),
+                       "note": "oracle/rt_oracle.c (the C restatement, lane-4 SSE, pthread tile queue, clang -O3 "
+                               "-mavx2 -mfma) on the same sample and cores"}
+        out["same_host_ratio_to_reference"] = round((p_rays / p_dt) / (rays / dt), 4)
+        out["within_10pct"] = bool(abs(out["same_host_ratio_to_reference"] - 1.0) <= 0.10)
+        out["same_host_ratio_single_thread"] = round((pp_rays / pp_dt) / (prays / pdt), 4)
+        out["frames_identical"] = bool(np.array_equal(cur, p_cur) and p_rays == rays)
+    calib = cpu_calibration()
     if calib:
-        # the reference cannot run on this box (/root/reference is absent): its speed relative to the
-        # port comes from the same-host record of the build container (scripts/cpu_calibrate.py)
-        out["same_host_ratio_to_reference"] = calib["same_host_ratio_to_reference"]
-        out["within_10pct"] = calib["within_10pct"]
+        # the build container's alternating-rounds record (scripts/cpu_calibrate.py)
+        if ref is None:
+            out["same_host_ratio_to_reference"] = calib["same_host_ratio_to_reference"]
+            out["within_10pct"] = calib["within_10pct"]
         out["calibration"] = {"source": calib["file"], "host_cpu": calib["host_cpu"],
                               "ratio_median_1_thread": calib["runs"]["1"]["ratio_median"],
                               "ratio_median_n_threads": {k: r["ratio_median"] for k, r in calib["runs"].items()
                                                          if k != "1"},
                               "note": "port / compiled reference (main.cpp:7-640, its own codegen flags) on the "
-                                      "same host and workload, frames identical; median of alternating rounds"}
+                                      "build container's host and the SURVEY 8d probe, frames identical; median of "
+                                      "alternating rounds"}
     return out
 
 
