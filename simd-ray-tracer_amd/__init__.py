@@ -436,7 +436,7 @@ class Device:
         keys = ["pri_iters", "pri_lanes", "sec_iters", "sec_lanes", "pri_groups", "sec_hit_groups",
                 "sec_sparse_iters", "sec_sparse_lanes", "sec_tail_iters", "pri_cycles", "sec_cycles",
                 "fold_cycles", "init_cycles", "cull_cycles", "sync_cycles", "post_cycles", "pf_iters", "pf_groups",
-                "pf_groups_noown", "pf_pairs", "pf_pairs_noown", "pf_lane_pairs", "pri_blocked", "pri_waitsec",
+                "cl_tested", "pf_pairs", "cl_top_entered", "pf_lane_pairs", "pri_blocked", "pri_waitsec",
                 "pri_done", "sec_done", "sec_waitpri", "done_trips", "done_lane_trips",
                 "sec_exact", "sec_badlanes", "sec_zerodir"]
         return {k: int(v) for k, v in zip(keys, out) if not k.startswith("_")}

@@ -132,7 +132,7 @@ enum { kWalkAny = 0, kWalkGroups, kWalkCl1, kWalkCl2, kWalkCl4, kWalkCl1Rel, kWa
 enum { kStatPriIters = 0, kStatPriLanes, kStatSecIters, kStatSecLanes, kStatPriGroups, kStatSecHitGroups,
        kStatSecSparseIters, kStatSecSparseLanes, kStatSecTailIters, kStatPriCycles, kStatSecCycles, kStatFoldCycles,
        kStatSetupCycles, kStatCullCycles, kStatSyncCycles, kStatPostCycles, kStatPfRounds, kStatPfGroups,
-       kStatPfGroupsNoOwn, kStatPfPairs, kStatPfPairsNoOwn, kStatPfLanePairs, kStatPriBlocked, kStatPriWaitSec,
+       kStatClTested, kStatPfPairs, kStatClTopEntered, kStatPfLanePairs, kStatPriBlocked, kStatPriWaitSec,
        kStatPriDone, kStatSecDone, kStatSecWaitPri, kStatDoneTrips, kStatDoneLaneTrips,
        kStatSecExact, kStatSecBadLanes, kStatSecZeroDir, kStatCount = 32 };
 constexpr uint32_t kStatSlots = 32;  // rt_debug_stats copies this many

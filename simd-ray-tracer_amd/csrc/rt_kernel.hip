@@ -217,7 +217,6 @@ struct Sample {
     float cx, cy, cz;  // output colour
     uint64_t rng;
     uint32_t bounce;
-    uint32_t own;      // RTK_STATS: sphere a diffuse outward bounce left (~0u: none)
 };
 
 // Jittered primary ray (main.cpp:375-385).
@@ -546,26 +545,17 @@ __device__ __forceinline__ void prefilter_group(const Group &G, const RayPk &p, 
 // group, and inside it one per flagged pair.  (Measured: +5.5 % on C2 over
 // one exact recheck of both pairs per flagged group.)
 struct PfStats {
-    uint32_t groups, groups_noown, pairs, pairs_noown, lane_pairs;
+    uint32_t groups, cl_tested, pairs, cl_top_entered, lane_pairs;
 };
 
 template <bool SIMD, bool GS, bool REL>
 __device__ __forceinline__ void test_group_pf(const TraceArgs &a, const float4 *lds_groups, const Group &G, uint32_t g,
-                                              const RayPk &p, Hit &h, uint32_t own = ~0u, PfStats *ps = nullptr) {
+                                              const RayPk &p, Hit &h, PfStats *ps = nullptr) {
     bool f01, f23;
     prefilter_group<REL>(G, p, f01, f23);
     if (ps) {
-        const bool mine = (own >> 2) == g;
-        const uint32_t ol = own & 3u;
-        f2 T01, T23, c01, c23;
-        const f2 e01 = pair_prefilter(p, f2{G.x[0], G.x[1]}, f2{G.y[0], G.y[1]}, f2{G.z[0], G.z[1]}, T01, c01);
-        const f2 e23 = pair_prefilter(p, f2{G.x[2], G.x[3]}, f2{G.y[2], G.y[3]}, f2{G.z[2], G.z[3]}, T23, c23);
-        const bool n01 = (!(e01.x >= G.r2p[0]) && !(mine && ol == 0u)) | (!(e01.y >= G.r2p[1]) && !(mine && ol == 1u));
-        const bool n23 = (!(e23.x >= G.r2p[2]) && !(mine && ol == 2u)) | (!(e23.y >= G.r2p[3]) && !(mine && ol == 3u));
         ps->groups += __ballot(f01 | f23) != 0;
-        ps->groups_noown += __ballot(n01 | n23) != 0;
         ps->pairs += (__ballot(f01) != 0) + (__ballot(f23) != 0);
-        ps->pairs_noown += (__ballot(n01) != 0) + (__ballot(n23) != 0);
         ps->lane_pairs += __builtin_popcountll(__ballot(f01)) + __builtin_popcountll(__ballot(f23));
     }
     if (f01 | f23) recheck_pairs<SIMD, GS>(a, lds_groups, G, g, p, h, f01, f23);
@@ -587,7 +577,7 @@ __device__ __forceinline__ Group load_group_pf_at(cv4f_t *cg) {
 // through the prefilter; else the exact test.
 template <bool SIMD, bool PF, bool GS, bool REL = false>
 __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4 *lds_groups, const RayPk &ray, Hit &h,
-                                                uint32_t *hit_groups, uint32_t own = ~0u, PfStats *ps = nullptr) {
+                                                uint32_t *hit_groups, PfStats *ps = nullptr) {
     cv4f_t *gp = (cv4f_t *)a.groups;
     // one group in SGPRs at a time: its s_load (scalar-cache hit) is covered
     // by the other waves on the SIMD -- measured as fast as a ping-pong
@@ -595,7 +585,7 @@ __device__ __forceinline__ void all_groups_smem(const TraceArgs &a, const float4
     // measured 2 % slower)
     for (uint32_t g = 0; g < a.n_groups; ++g, gp += kGroupF4) {
         const Group G = PF ? load_group_pf_at(gp) : load_group_at(gp);
-        if (PF) test_group_pf<SIMD, GS, REL>(a, lds_groups, G, g, ray, h, own, ps);
+        if (PF) test_group_pf<SIMD, GS, REL>(a, lds_groups, G, g, ray, h, ps);
         else test_group<SIMD>(a, G, g, ray, h, hit_groups);
     }
 }
@@ -676,9 +666,55 @@ __device__ __forceinline__ cv4f_t *opaque(cv4f_t *p) {
     return p;
 }
 
+// The per-lane thresholds of per-lane (REL) tables, both members of an entry
+// per packed FMA.  The constants sit in VGPR pairs (kc = {kClRel, kBehindRel},
+// kp = {kPfRel, kSlabRel}, aux = {slab_e0, |D.y|}) and op_sel broadcasts one
+// half to both lanes: an f32 FMA with a literal and an SGPR row lowered to
+// v_mov + v_fmamk, two VALU per threshold where this is half of one.  Every
+// value is the same single-rounded FMA as fmaf, so the bits are unchanged.
+struct ClConst {
+    f2 kc, kp, aux;
+};
+
+// A constant in a VGPR, written where the walk starts: a plain constant is
+// hoisted to the kernel's entry and held across every loop, which pushed other
+// values into scratch.
+__device__ __forceinline__ float walk_const(float c) {
+    float r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(c));
+    return r;
+}
+
+// t = cc * kPfRel + r (a member pair's near-line thresholds)
+__device__ __forceinline__ f2 member_thr(f2 cc, const ClConst &k, f2 r) {
+    f2 t;
+    asm("v_pk_fma_f32 %[t], %[cc], %[kp], %[r] op_sel_hi:[1,0,1]" : [t] "=v"(t) : [cc] "v"(cc), [kp] "v"(k.kp), [r] "s"(r));
+    return t;
+}
+
+// A cluster pair's near-line thresholds t = cc kClRel + R, behind bounds
+// b = beta - cc kBehindRel, and the height-slab distance d = |O.y + D.y T - ymid|
+// (before the abs) with its limit thr = |D.y| srho + (yhalf + E),
+// E = cc kSlabRel + slab_e0 (cluster_pair below).
+__device__ __forceinline__ void cluster_thr(f2 cc, f2 T, const RayPk &ray, const ClConst &k, f2 r, f2 beta, f2 srho,
+                                            f2 ymid, f2 yhalf, f2 &t, f2 &b, f2 &d, f2 &thr) {
+    asm("v_pk_fma_f32 %[t], %[cc], %[kc], %[r] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[b], %[cc], %[kc], %[beta] op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[0,1,0] neg_hi:[0,1,0]"
+        : [t] "=&v"(t), [b] "=&v"(b)
+        : [cc] "v"(cc), [kc] "v"(k.kc), [r] "s"(r), [beta] "s"(beta));
+    asm("v_pk_fma_f32 %[thr], %[cc], %[kp], %[aux] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
+        "v_pk_add_f32 %[thr], %[yhalf], %[thr]\n\t"
+        "v_pk_fma_f32 %[thr], %[aux], %[srho], %[thr] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[d], %[ry], %[T], %[ry] op_sel:[1,0,0] op_sel_hi:[1,1,0]\n\t"
+        "v_pk_add_f32 %[d], %[d], %[ymid] neg_lo:[0,1] neg_hi:[0,1]"
+        : [thr] "=&v"(thr), [d] "=&v"(d)
+        : [cc] "v"(cc), [kp] "v"(k.kp), [aux] "v"(k.aux), [yhalf] "s"(yhalf), [srho] "s"(srho), [ry] "v"(ray.y),
+          [T] "v"(T), [ymid] "s"(ymid));
+}
+
 template <int W, bool REL>
 __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_t count, const RayPk &ray,
-                                             uint64_t (&wave)[kClWords], PfStats *ps) {
+                                             uint64_t (&wave)[kClWords], const ClConst &k, PfStats *ps) {
     constexpr uint32_t kEntryBytes = 16u * cl_entry_f4(W, REL);
     if (ps) ps->groups += count;
     const uint32_t end = (first + count) * kEntryBytes;
@@ -690,8 +726,8 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
         f2 T, cc;
         const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
         // a lane may hit the sphere: near the line, and not wholly behind the origin
-        const float t0 = REL ? __builtin_fmaf(cc.x, kPfRel, r1.z) : r1.z;
-        const float t1 = REL ? __builtin_fmaf(cc.y, kPfRel, r1.w) : r1.w;
+        const f2 tr = REL ? member_thr(cc, k, f2{r1.z, r1.w}) : f2{r1.z, r1.w};
+        const float t0 = tr.x, t1 = tr.y;
         const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
         const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
         // Members of per-lane (REL) tables take the near-line test only: their behind
@@ -736,37 +772,34 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
 // One cluster-pair entry (both levels of the table share the row layout):
 // the wave's lanes that may reach cluster 0 / 1 (near the line, not wholly
 // behind the origin, and for per-lane tables inside the height slab).
-template <bool REL, bool SLAB = REL>
-__device__ __forceinline__ void cluster_pair(cv4f_t *e, const RayPk &ray, float oy, float dy, float slab_e0,
-                                             uint64_t &m0, uint64_t &m1) {
+// Height slab (per-lane tables): the line's height over the t range that can
+// reach the cluster is c +- |D.y| srho with c = O.y + D.y T; it cannot meet a
+// member when that range clears [ymid - yhalf, ymid + yhalf] by the lane's
+// margin E (a ground-plane scene: rays leaving the ground cross the thin layer
+// of small spheres only near their origin).
+template <bool REL>
+__device__ __forceinline__ void cluster_pair(cv4f_t *e, const RayPk &ray, const ClConst &k, uint64_t &m0,
+                                             uint64_t &m1) {
     const v4f_t r0 = e[0], r1 = e[1], r3 = e[3];
     f2 T, cc;
     const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
-    const float t0 = REL ? __builtin_fmaf(cc.x, kClRel, r1.z) : r1.z;
-    const float t1 = REL ? __builtin_fmaf(cc.y, kClRel, r1.w) : r1.w;
-    const float b0 = REL ? __builtin_fmaf(cc.x, -kBehindRel, r3.x) : r3.x;
-    const float b1 = REL ? __builtin_fmaf(cc.y, -kBehindRel, r3.y) : r3.y;
-    m0 = ballot_and(!(v.x >= t0), !(T.x < b0));
-    m1 = ballot_and(!(v.y >= t1), !(T.y < b1));
-    if constexpr (REL && SLAB) {
-        // Height slab: the line's height over the t range that can reach the
-        // cluster is c +- |D.y| srho with c = O.y + D.y T; it cannot meet a
-        // member when that range clears [ymid - yhalf, ymid + yhalf] by the
-        // lane's margin E (a ground-plane scene: rays leaving the ground cross the
-        // thin layer of small spheres only near their origin).
+    if constexpr (REL) {
         const v4f_t r4 = e[4];
-        const f2 E = __builtin_elementwise_fma(cc, f2{kSlabRel, kSlabRel}, f2{slab_e0, slab_e0});
-        const f2 c = __builtin_elementwise_fma(f2{dy, dy}, T, f2{oy, oy});
-        const f2 d = c - f2{r4.x, r4.y};
-        const f2 thr = __builtin_elementwise_fma(f2{__builtin_fabsf(dy), __builtin_fabsf(dy)}, f2{r3.z, r3.w},
-                                                 f2{r4.z, r4.w} + E);
-        m0 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
-        m1 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
+        f2 t, b, d, thr;
+        cluster_thr(cc, T, ray, k, f2{r1.z, r1.w}, f2{r3.x, r3.y}, f2{r3.z, r3.w}, f2{r4.x, r4.y}, f2{r4.z, r4.w}, t,
+                    b, d, thr);
+        m0 = ballot_and(!(v.x >= t.x), !(T.x < b.x)) & __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
+        m1 = ballot_and(!(v.y >= t.y), !(T.y < b.y)) & __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
+    } else {
+        m0 = ballot_and(!(v.x >= r1.z), !(T.x < r3.x));
+        m1 = ballot_and(!(v.y >= r1.w), !(T.y < r3.y));
     }
 }
 
 // ps (RTK_STATS): groups += member-pair entries tested, pairs += sphere pairs
-// rechecked exactly, lane_pairs += clusters entered (per wave, both levels).
+// rechecked exactly, lane_pairs += clusters entered (per wave, both levels),
+// cl_tested += cluster-pair entries tested (both levels), cl_top_entered += top
+// clusters entered (two-level tables).
 // Tables of two or more mask words (more than 32 groups) have two levels: a
 // top cluster's entry ranges index sub-cluster entries of a few spheres each,
 // whose ranges index the member entries (rt_host.cpp cluster_table); the bound
@@ -782,29 +815,38 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
     // per-lane part of the height-slab margin (REL tables; rt_host.cpp cluster_table)
     const float oy = ray.y.x, dy = ray.y.y;
     const float slab_e0 = REL ? __builtin_fmaf(__builtin_fabsf(oy), 0x1p-21f, kSlabRel) : 0.0f;
+    ClConst k;
+    if constexpr (REL) {
+        k.kc = f2{walk_const(kClRel), walk_const(kBehindRel)};
+        k.kp = f2{walk_const(kPfRel), walk_const(kSlabRel)};
+        k.aux = f2{slab_e0, __builtin_fabsf(dy)};
+    }
     // the member pairs of an entered (sub-)cluster pair entry
     auto members = [&](cv4f_t *e, bool in0, bool in1) {
         const v4f_t r2 = e[2];
         if (ps) ps->lane_pairs += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
-        if (in0) member_pairs<W, REL>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, ps);
-        if (in1) member_pairs<W, REL>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, ps);
+        if (in0) member_pairs<W, REL>(ct, __float_as_uint(r2.x), __float_as_uint(r2.y), ray, wave, k, ps);
+        if (in1) member_pairs<W, REL>(ct, __float_as_uint(r2.z), __float_as_uint(r2.w), ray, wave, k, ps);
     };
     // the sub-cluster pair entries [first, first + count) of an entered top cluster
     auto subs = [&](uint32_t first, uint32_t count) {
+        if (ps) ps->cl_tested += count;
         for (uint32_t off = first * kEntryBytes, end = (first + count) * kEntryBytes; off != end; off += kEntryBytes) {
             cv4f_t *e = cl_entry(ct, off);
             uint64_t m0, m1;
-            cluster_pair<REL>(e, ray, oy, dy, slab_e0, m0, m1);
+            cluster_pair<REL>(e, ray, k, m0, m1);
             members(e, m0 != 0, m1 != 0);
         }
     };
+    if (ps) ps->cl_tested += a.n_cpairs;
     for (uint32_t off = 0, end = a.n_cpairs * kEntryBytes; off != end; off += kEntryBytes) {
         cv4f_t *e = cl_entry(ct, off);
         uint64_t m0, m1;
-        cluster_pair<REL>(e, ray, oy, dy, slab_e0, m0, m1);
+        cluster_pair<REL>(e, ray, k, m0, m1);
         if constexpr (kTwoLevels) {
             const v4f_t r2 = e[2];
             if (ps) ps->lane_pairs += (m0 != 0 ? 1u : 0u) + (m1 != 0 ? 1u : 0u);
+            if (ps) ps->cl_top_entered += (m0 != 0 ? 1u : 0u) + (m1 != 0 ? 1u : 0u);
             if (m0 != 0) subs(__float_as_uint(r2.x), __float_as_uint(r2.y));
             if (m1 != 0) subs(__float_as_uint(r2.z), __float_as_uint(r2.w));
         } else {
@@ -1274,7 +1316,6 @@ void trace_kernel(TraceArgs a) {
     uint32_t st_pf_rounds = 0;
     Sample p;
     p.bounce = 0;
-    p.own = ~0u;
     p.cx = p.cy = p.cz = 0.0f;
 
     // Empty tile: no sphere group passes the tile's (conservative) cone test,
@@ -1347,7 +1388,6 @@ void trace_kernel(TraceArgs a) {
         const float4 cs = rec[1];
         const float4 ei = rec[2];
         shade(lut, cs, ei, hx, hy, hz, inside, p);
-        if (kStats) p.own = (ei.w == 0.0f && !inside) ? sidx : ~0u;
         p.bounce += 1;
     };
     // the pixel's owner lane's fold cursor (first of its P-lane slice) via DPP
@@ -1561,11 +1601,11 @@ void trace_kernel(TraceArgs a) {
                             }
                         } else if (SRC == kSrcSmem && pf && a.pf_relative && !Walk<WALK>::CLUSTERS) {
                             if (kStats && a.stats) st_pf_rounds += 1;
-                            all_groups_smem<SIMD, true, GS, true>(a, lds_groups, ray, h, nullptr, p.own,
+                            all_groups_smem<SIMD, true, GS, true>(a, lds_groups, ray, h, nullptr,
                                                                   kStats && a.stats ? &st_pf : nullptr);
                         } else if (SRC == kSrcSmem && pf && !Walk<WALK>::CLUSTERS) {
                             if (kStats && a.stats) st_pf_rounds += 1;
-                            all_groups_smem<SIMD, true, GS>(a, lds_groups, ray, h, nullptr, p.own,
+                            all_groups_smem<SIMD, true, GS>(a, lds_groups, ray, h, nullptr,
                                                         kStats && a.stats ? &st_pf : nullptr);
                         } else if (SRC == kSrcSmem) {
                             all_groups_smem<SIMD, false, GS>(a, lds_groups, ray, h,
@@ -1715,9 +1755,9 @@ void trace_kernel(TraceArgs a) {
         atomicAdd(a.stats + kStatPostCycles, (unsigned long long)st_cyc_post);
         atomicAdd(a.stats + kStatPfRounds, (unsigned long long)st_pf_rounds);
         atomicAdd(a.stats + kStatPfGroups, (unsigned long long)st_pf.groups);
-        atomicAdd(a.stats + kStatPfGroupsNoOwn, (unsigned long long)st_pf.groups_noown);
+        atomicAdd(a.stats + kStatClTested, (unsigned long long)st_pf.cl_tested);
         atomicAdd(a.stats + kStatPfPairs, (unsigned long long)st_pf.pairs);
-        atomicAdd(a.stats + kStatPfPairsNoOwn, (unsigned long long)st_pf.pairs_noown);
+        atomicAdd(a.stats + kStatClTopEntered, (unsigned long long)st_pf.cl_top_entered);
         atomicAdd(a.stats + kStatPfLanePairs, (unsigned long long)st_pf.lane_pairs);
         atomicAdd(a.stats + kStatPriBlocked, (unsigned long long)st_pri_blocked);
         atomicAdd(a.stats + kStatPriWaitSec, (unsigned long long)st_pri_waitsec);
