@@ -2,6 +2,7 @@
 // trace kernel, against the compiler's IEEE sequences (-ffp-contract=off):
 //   rcp:  y = RN(1/b) from v_rcp_f32 + one Newton step       (exhaustive mantissas x exponent range)
 //   sqrt: RN(sqrt(x)) from v_sqrt_f32 + +-1ulp residual fix   (exhaustive mantissas x exponent range)
+//         and from v_rsq_f32 + one fma correction (Markstein; the kernel's sqrt_rn since round 6, mode 6)
 //   div:  RN(a/b) = fma(r, y, q0), q0 = a*y, r = fma(-q0, b, a), y = RN(1/b)  (random + edge pairs)
 // Prints mismatch counts and the first few mismatching inputs.
 #include <hip/hip_runtime.h>
@@ -31,6 +32,27 @@ __device__ __forceinline__ float sqrt_up(float x) {  // the residual fix away fr
     const float sp = __uint_as_float(__float_as_uint(s) + 1u);
     return __builtin_fmaf(-sp, s, x) > 0.0f ? sp : s;
 }
+__device__ __forceinline__ float sqrt_markstein(float x) {  // v_rsq_f32 + one fma correction
+    const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);  // x = 0 -> 0
+    const float g = x * y, h = 0.5f * y;
+    const float r = __builtin_fmaf(-g, g, x);
+    return __builtin_fmaf(r, h, g);
+}
+__device__ __forceinline__ float sqrt_markstein2(float x) {  // v_rsq_f32, one Goldschmidt step, then the correction
+    const float y = __builtin_amdgcn_rsqf(x);
+    float g = x * y, h = 0.5f * y;
+    const float e = __builtin_fmaf(-g, h, 0.5f);
+    g = __builtin_fmaf(g, e, g);
+    h = __builtin_fmaf(h, e, h);
+    const float r = __builtin_fmaf(-g, g, x);
+    return __builtin_fmaf(r, h, g);
+}
+__device__ __forceinline__ float sqrt_vsqrt_fma(float x) {  // v_sqrt_f32 + one correction with h = 0.5 v_rsq
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float h = 0.5f * __builtin_amdgcn_rsqf(x);
+    const float r = __builtin_fmaf(-s, s, x);
+    return __builtin_fmaf(r, h, s);
+}
 __device__ __forceinline__ float div_fast(float a, float b, float y) {
     const float q0 = a * y;
     const float r = __builtin_fmaf(-q0, b, a);
@@ -56,6 +78,9 @@ __global__ void k_unary(int mode, int e0, unsigned long long *cnt, uint32_t *bad
     else if (mode == 2) { got = __builtin_amdgcn_sqrtf(x); want = __builtin_sqrtf(x); }   // raw v_sqrt_f32
     else if (mode == 3) { got = sqrt_down(x); want = __builtin_sqrtf(x); }               // only the -1ulp fix
     else if (mode == 4) { got = sqrt_up(x); want = __builtin_sqrtf(x); }                 // only the +1ulp fix
+    else if (mode == 6) { got = sqrt_markstein(x); want = __builtin_sqrtf(x); }
+    else if (mode == 7) { got = sqrt_markstein2(x); want = __builtin_sqrtf(x); }
+    else if (mode == 8) { got = sqrt_vsqrt_fma(x); want = __builtin_sqrtf(x); }
     else { got = __builtin_amdgcn_rcpf(x); want = 1.0f / x; }                            // raw v_rcp_f32
     if (__float_as_uint(got) != __float_as_uint(want)) report(cnt, bad, u, 0);
 }
@@ -127,6 +152,12 @@ int main() {
     run("sqrt raw v_sqrt_f32, 2^-60..2^60", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 2, 67, cnt, bad); });
     run("sqrt v_sqrt + down fix only", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 3, 67, cnt, bad); });
     run("sqrt v_sqrt + up fix only", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 4, 67, cnt, bad); });
+    run("sqrt v_rsq + fma correction", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 6, 67, cnt, bad); });
+    // the whole normal range 2^-126 .. 2^128 (exponents 1..254): beyond the kernel's proven callers
+    run("sqrt v_rsq + fma correction, all normals", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 254), dim3(256), 0, 0, 6, 1, cnt, bad); });
+    run("sqrt v_sqrt+fix, all normals", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 254), dim3(256), 0, 0, 1, 1, cnt, bad); });
+    run("sqrt v_rsq + Goldschmidt + correction", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 7, 67, cnt, bad); });
+    run("sqrt v_sqrt + fma correction (rsq h)", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 8, 67, cnt, bad); });
     run("rcp  raw v_rcp_f32, 2^-40..2^40", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 80), dim3(256), 0, 0, 5, 87, cnt, bad); });
     // b in [2^-8, 2^8), a in [2^-40, 2^24): quotients 2^-48 .. 2^32 (normal)
     for (int rep = 0; rep < 4; ++rep)

@@ -77,15 +77,23 @@ __device__ __forceinline__ float rcp_rn(float b) {
     return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
 }
 
-// RN(sqrt(x)) for x = 0 or x in [2^-60, 2^60]: v_sqrt_f32 (< 1 ulp) and
-// the +-1 ulp residual test (the compiler's sequence minus its
-// denormal/infinity range scaling).
-// RTK_SQRT_FIX (experiment builds only, scripts/mathcheck.hip decides): 2 = both
-// residual tests, 1 = the -1 ulp test only, 3 = the +1 ulp test only, 0 = none.
+// RN(sqrt(x)) for x = 0 or x in [2^-60, 2^60] (Markstein): y = v_rsq_f32(x),
+// g = RN(x y), h = y / 2, r = x - g^2 (one fma, exact), result RN(g + r h).
+// scripts/mathcheck.hip finds it bit-identical to the IEEE sqrt on every f32 of
+// the range (mode 6, profiles/r06q_mathcheck.txt).  x = 0: v_rsq gives +inf,
+// clamped to 2^64 so g = 0 and the result is +0 (the range's y is below 2^30).
+// Five full-rate ops besides the transcendental, against eight for v_sqrt_f32
+// and its two +-1 ulp residual tests (round 5's form, RTK_SQRT_FIX=2 in
+// experiment builds): C2 +2.5 %, RTWeekend +2.3 % (profiles/r06q_sqrt_ab.txt).
 #ifndef RTK_SQRT_FIX
-#define RTK_SQRT_FIX 2
+#define RTK_SQRT_FIX 4
 #endif
 __device__ __forceinline__ float sqrt_rn(float x) {
+    if (RTK_SQRT_FIX == 4) {
+        const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
+        const float g = x * y, h = 0.5f * y;
+        return __builtin_fmaf(__builtin_fmaf(-g, g, x), h, g);
+    }
     const float s = __builtin_amdgcn_sqrtf(x);
     const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
     float r = s;
@@ -696,12 +704,14 @@ __device__ __forceinline__ f2 member_thr(f2 cc, const ClConst &k, f2 r) {
 // b = beta - cc kBehindRel, and the height-slab distance d = |O.y + D.y T - ymid|
 // (before the abs) with its limit thr = |D.y| srho + (yhalf + E),
 // E = cc kSlabRel + slab_e0 (cluster_pair below).
-__device__ __forceinline__ void cluster_thr(f2 cc, f2 T, const RayPk &ray, const ClConst &k, f2 r, f2 beta, f2 srho,
-                                            f2 ymid, f2 yhalf, f2 &t, f2 &b, f2 &d, f2 &thr) {
+__device__ __forceinline__ void cluster_thr(f2 cc, const ClConst &k, f2 r, f2 beta, f2 &t, f2 &b) {
     asm("v_pk_fma_f32 %[t], %[cc], %[kc], %[r] op_sel_hi:[1,0,1]\n\t"
         "v_pk_fma_f32 %[b], %[cc], %[kc], %[beta] op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[0,1,0] neg_hi:[0,1,0]"
         : [t] "=&v"(t), [b] "=&v"(b)
         : [cc] "v"(cc), [kc] "v"(k.kc), [r] "s"(r), [beta] "s"(beta));
+}
+__device__ __forceinline__ void cluster_slab(f2 cc, f2 T, const RayPk &ray, const ClConst &k, f2 srho, f2 ymid,
+                                             f2 yhalf, f2 &d, f2 &thr) {
     asm("v_pk_fma_f32 %[thr], %[cc], %[kp], %[aux] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
         "v_pk_add_f32 %[thr], %[yhalf], %[thr]\n\t"
         "v_pk_fma_f32 %[thr], %[aux], %[srho], %[thr] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
@@ -777,19 +787,29 @@ __device__ __forceinline__ void member_pairs(cv4f_t *ct, uint32_t first, uint32_
 // member when that range clears [ymid - yhalf, ymid + yhalf] by the lane's
 // margin E (a ground-plane scene: rays leaving the ground cross the thin layer
 // of small spheres only near their origin).
-template <bool REL>
+template <bool REL, bool SLAB = true, bool BEHIND = true>
 __device__ __forceinline__ void cluster_pair(cv4f_t *e, const RayPk &ray, const ClConst &k, uint64_t &m0,
                                              uint64_t &m1) {
     const v4f_t r0 = e[0], r1 = e[1], r3 = e[3];
     f2 T, cc;
     const f2 v = pair_prefilter(ray, f2{r0.x, r0.y}, f2{r0.z, r0.w}, f2{r1.x, r1.y}, T, cc);
     if constexpr (REL) {
-        const v4f_t r4 = e[4];
-        f2 t, b, d, thr;
-        cluster_thr(cc, T, ray, k, f2{r1.z, r1.w}, f2{r3.x, r3.y}, f2{r3.z, r3.w}, f2{r4.x, r4.y}, f2{r4.z, r4.w}, t,
-                    b, d, thr);
-        m0 = ballot_and(!(v.x >= t.x), !(T.x < b.x)) & __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
-        m1 = ballot_and(!(v.y >= t.y), !(T.y < b.y)) & __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
+        f2 t, b;
+        cluster_thr(cc, k, f2{r1.z, r1.w}, f2{r3.x, r3.y}, t, b);
+        if (BEHIND) {
+            m0 = ballot_and(!(v.x >= t.x), !(T.x < b.x));
+            m1 = ballot_and(!(v.y >= t.y), !(T.y < b.y));
+        } else {
+            m0 = __builtin_amdgcn_ballot_w64(!(v.x >= t.x));
+            m1 = __builtin_amdgcn_ballot_w64(!(v.y >= t.y));
+        }
+        if constexpr (SLAB) {
+            const v4f_t r4 = e[4];
+            f2 d, thr;
+            cluster_slab(cc, T, ray, k, f2{r3.z, r3.w}, f2{r4.x, r4.y}, f2{r4.z, r4.w}, d, thr);
+            m0 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.x) > thr.x));
+            m1 &= __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(d.y) > thr.y));
+        }
     } else {
         m0 = ballot_and(!(v.x >= r1.z), !(T.x < r3.x));
         m1 = ballot_and(!(v.y >= r1.w), !(T.y < r3.y));
@@ -834,7 +854,10 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
         for (uint32_t off = first * kEntryBytes, end = (first + count) * kEntryBytes; off != end; off += kEntryBytes) {
             cv4f_t *e = cl_entry(ct, off);
             uint64_t m0, m1;
-            cluster_pair<REL>(e, ray, k, m0, m1);
+#ifndef RTK_EXP_SUB
+#define RTK_EXP_SUB true, true
+#endif
+            cluster_pair<REL, RTK_EXP_SUB>(e, ray, k, m0, m1);
             members(e, m0 != 0, m1 != 0);
         }
     };
@@ -842,7 +865,10 @@ __device__ __forceinline__ void clustered_groups(const TraceArgs &a, const float
     for (uint32_t off = 0, end = a.n_cpairs * kEntryBytes; off != end; off += kEntryBytes) {
         cv4f_t *e = cl_entry(ct, off);
         uint64_t m0, m1;
-        cluster_pair<REL>(e, ray, k, m0, m1);
+#ifndef RTK_EXP_TOP
+#define RTK_EXP_TOP true, true
+#endif
+        cluster_pair<REL, RTK_EXP_TOP>(e, ray, k, m0, m1);
         if constexpr (kTwoLevels) {
             const v4f_t r2 = e[2];
             if (ps) ps->lane_pairs += (m0 != 0 ? 1u : 0u) + (m1 != 0 ? 1u : 0u);
