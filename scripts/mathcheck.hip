@@ -79,6 +79,12 @@ __global__ void k_unary(int mode, int e0, unsigned long long *cnt, uint32_t *bad
     else if (mode == 3) { got = sqrt_down(x); want = __builtin_sqrtf(x); }               // only the -1ulp fix
     else if (mode == 4) { got = sqrt_up(x); want = __builtin_sqrtf(x); }                 // only the +1ulp fix
     else if (mode == 6) { got = sqrt_markstein(x); want = __builtin_sqrtf(x); }
+    else if (mode == 9) {  // RN(1/len), len = RN(sqrt(x)), by one Newton step from v_rsq_f32(x) (normalize's reciprocal)
+        const float len = sqrt_markstein(x);
+        const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
+        got = __builtin_fmaf(__builtin_fmaf(-len, y, 1.0f), y, y);
+        want = 1.0f / len;
+    }
     else if (mode == 7) { got = sqrt_markstein2(x); want = __builtin_sqrtf(x); }
     else if (mode == 8) { got = sqrt_vsqrt_fma(x); want = __builtin_sqrtf(x); }
     else { got = __builtin_amdgcn_rcpf(x); want = 1.0f / x; }                            // raw v_rcp_f32
@@ -154,6 +160,7 @@ int main() {
     run("sqrt v_sqrt + up fix only", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 4, 67, cnt, bad); });
     run("sqrt v_rsq + fma correction", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 6, 67, cnt, bad); });
     // the whole normal range 2^-126 .. 2^128 (exponents 1..254): beyond the kernel's proven callers
+    run("rcp  1/RN(sqrt x) by Newton from v_rsq(x), 2^-60..2^100", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 160), dim3(256), 0, 0, 9, 67, cnt, bad); });
     run("sqrt v_rsq + fma correction, all normals", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 254), dim3(256), 0, 0, 6, 1, cnt, bad); });
     run("sqrt v_sqrt+fix, all normals", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 254), dim3(256), 0, 0, 1, 1, cnt, bad); });
     run("sqrt v_rsq + Goldschmidt + correction", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 7, 67, cnt, bad); });
