@@ -400,6 +400,16 @@ static void put_material(float *dst, const rt_material &m) {
     dst[5] = m.Emissive.y;
     dst[6] = m.Emissive.z;
     dst[7] = m.IndexOfRefraction;
+    // row 3: the dielectric path's per-material quotients, the reference's own f32 divisions done
+    // once here (IEEE, as the kernel's were): eta outside = 1/IOR (main.cpp:463) and Reflectance's
+    // r0 = ((1 - eta)/(1 + eta))^2 (main.cpp:292-295) for eta outside and inside (= IOR)
+    if (m.IndexOfRefraction != 0.0f) {
+        const float ior = m.IndexOfRefraction, eo = 1.0f / ior;
+        const float ro = (1.0f - eo) / (1.0f + eo), ri = (1.0f - ior) / (1.0f + ior);
+        dst[8] = eo;
+        dst[9] = ro * ro;
+        dst[10] = ri * ri;
+    }
 }
 
 // Prefilter thresholds r2p (row 4 of each group) for the secondary-ray

@@ -44,7 +44,8 @@ constexpr uint32_t kClAutoGroups = 128;  // used by default up to this many (rt_
 //               r2p = prefilter threshold of the secondary-ray sphere loop (rt_host.cpp);
 //               with pf_relative, r*r again (-inf: never hit) and the threshold is formed per lane
 //   spheres   : 4*n_groups records of kSphereF4 float4 = {centre.xyz, 0}, {Color.xyz, Specular},
-//               {Emissive.xyz, IOR}, {0} (64 B/sphere: what shading gathers for the winning sphere,
+//               {Emissive.xyz, IOR}, {1/IOR, r0 outside, r0 inside, 0} (dielectrics; else 0)
+//               (64 B/sphere: what shading gathers for the winning sphere,
 //               addressed by one shift of its index; TraceArgs.materials)
 // r*r is precomputed on the host with the same f32 multiply the reference
 // repeats per test (main.cpp:406), so it is bit-identical.

@@ -209,9 +209,17 @@ __device__ __forceinline__ uint32_t rgba8(float x, float y, float z, bool pw) {
            (255u << 24);
 }
 
-__device__ __forceinline__ float reflectance(float cos_t, float eta) {  // main.cpp:292-300
-    float r0 = (1.0f - eta) / (1.0f + eta);
-    r0 *= r0;
+#ifndef RTK_DIEL_TAB
+#define RTK_DIEL_TAB 0
+#endif
+// r0 = ((1 - eta)/(1 + eta))^2 comes from the sphere record (the host's IEEE
+// division, rt_host.cpp put_material) when RTK_DIEL_TAB
+__device__ __forceinline__ float reflectance(float cos_t, float eta, float r0_tab) {  // main.cpp:292-300
+    float r0 = r0_tab;
+    if (!RTK_DIEL_TAB) {
+        r0 = (1.0f - eta) / (1.0f + eta);
+        r0 *= r0;
+    }
     float r1 = 1.0f - cos_t;
     r1 = r1 * r1 * r1 * r1 * r1;
     return __builtin_fmaf(1.0f - r0, r1, r0);  // contracted by the reference's -mfma build
@@ -268,8 +276,8 @@ __device__ __forceinline__ void start_sample(const Args &a, uint32_t x, uint32_t
 }
 
 // Emission, attenuation and the next direction (main.cpp:446-481).
-__device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 emis_ior, float hx, float hy, float hz,
-                                      bool inside, Sample &p) {
+__device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 emis_ior, const float4 *diel, float hx,
+                                      float hy, float hz, bool inside, Sample &p) {
     p.cx = p.cx + emis_ior.x * p.ax;
     p.cy = p.cy + emis_ior.y * p.ay;
     p.cz = p.cz + emis_ior.z * p.az;
@@ -306,7 +314,9 @@ __device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 em
         p.ry.y = dy;
         p.rz.y = dz;
     } else {
-        const float eta = inside ? ior : 1.0f / ior;
+        // {1/IOR, r0 outside, r0 inside} of the record's row 3 (dielectric lanes only)
+        const float4 dq = RTK_DIEL_TAB ? *diel : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float eta = inside ? ior : RTK_DIEL_TAB ? dq.x : 1.0f / ior;
         const float dd = dot3(-p.rx.y, -p.ry.y, -p.rz.y, nx, ny, nz);
         const float cos_t = dd < 1.0f ? dd : 1.0f;  // _mm_min_ss
         // 1 - c*c and |1 - q.q| are 0 or >= 2^-25 (or NaN): inside sqrt_rn's range
@@ -319,7 +329,7 @@ __device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 em
         float rx = qx + q * nx, ry = qy + q * ny, rz = qz + q * nz;
         normalize(rx, ry, rz);
         bool refl = cant;
-        if (!refl) refl = reflectance(cos_t, eta) > rand_float(p.rng, 0.0f, kInvRange1);
+        if (!refl) refl = reflectance(cos_t, eta, inside ? dq.z : dq.y) > rand_float(p.rng, 0.0f, kInvRange1);
         if (refl && !inside) {
             p.rx.y = bx;
             p.ry.y = by;
@@ -1413,7 +1423,7 @@ void trace_kernel(TraceArgs a) {
         p.rz.x = p.rz.x + ipz;
         const float4 cs = rec[1];
         const float4 ei = rec[2];
-        shade(lut, cs, ei, hx, hy, hz, inside, p);
+        shade(lut, cs, ei, rec + 3, hx, hy, hz, inside, p);
         p.bounce += 1;
     };
     // the pixel's owner lane's fold cursor (first of its P-lane slice) via DPP
