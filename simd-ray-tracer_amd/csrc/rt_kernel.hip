@@ -209,17 +209,11 @@ __device__ __forceinline__ uint32_t rgba8(float x, float y, float z, bool pw) {
            (255u << 24);
 }
 
-#ifndef RTK_DIEL_TAB
-#define RTK_DIEL_TAB 0
-#endif
-// r0 = ((1 - eta)/(1 + eta))^2 comes from the sphere record (the host's IEEE
-// division, rt_host.cpp put_material) when RTK_DIEL_TAB
-__device__ __forceinline__ float reflectance(float cos_t, float eta, float r0_tab) {  // main.cpp:292-300
-    float r0 = r0_tab;
-    if (!RTK_DIEL_TAB) {
-        r0 = (1.0f - eta) / (1.0f + eta);
-        r0 *= r0;
-    }
+// r0 = ((1 - eta)/(1 + eta))^2 comes from the sphere record: the host's IEEE
+// division and product per material and side (rt_host.cpp put_material), the
+// same bits as the kernel's own (RTWeekend +0.4 %, its 8-rank share +1.3 %,
+// profiles/r06s_diel_tab_ab.txt)
+__device__ __forceinline__ float reflectance(float cos_t, float r0) {  // main.cpp:292-300
     float r1 = 1.0f - cos_t;
     r1 = r1 * r1 * r1 * r1 * r1;
     return __builtin_fmaf(1.0f - r0, r1, r0);  // contracted by the reference's -mfma build
@@ -315,8 +309,8 @@ __device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 em
         p.rz.y = dz;
     } else {
         // {1/IOR, r0 outside, r0 inside} of the record's row 3 (dielectric lanes only)
-        const float4 dq = RTK_DIEL_TAB ? *diel : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float eta = inside ? ior : RTK_DIEL_TAB ? dq.x : 1.0f / ior;
+        const float4 dq = *diel;
+        const float eta = inside ? ior : dq.x;
         const float dd = dot3(-p.rx.y, -p.ry.y, -p.rz.y, nx, ny, nz);
         const float cos_t = dd < 1.0f ? dd : 1.0f;  // _mm_min_ss
         // 1 - c*c and |1 - q.q| are 0 or >= 2^-25 (or NaN): inside sqrt_rn's range
@@ -329,7 +323,7 @@ __device__ __forceinline__ void shade(const Lut &lut, float4 col_spec, float4 em
         float rx = qx + q * nx, ry = qy + q * ny, rz = qz + q * nz;
         normalize(rx, ry, rz);
         bool refl = cant;
-        if (!refl) refl = reflectance(cos_t, eta, inside ? dq.z : dq.y) > rand_float(p.rng, 0.0f, kInvRange1);
+        if (!refl) refl = reflectance(cos_t, inside ? dq.z : dq.y) > rand_float(p.rng, 0.0f, kInvRange1);
         if (refl && !inside) {
             p.rx.y = bx;
             p.ry.y = by;
