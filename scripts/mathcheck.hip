@@ -85,6 +85,13 @@ __global__ void k_unary(int mode, int e0, unsigned long long *cnt, uint32_t *bad
         got = __builtin_fmaf(__builtin_fmaf(-len, y, 1.0f), y, y);
         want = 1.0f / len;
     }
+    else if (mode == 10) {  // mode 9 with the kernel's fallback: len's mantissa all ones -> rcp + Newton
+        const float len = sqrt_markstein(x);
+        const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
+        got = __builtin_fmaf(__builtin_fmaf(-len, y, 1.0f), y, y);
+        if ((__float_as_uint(len) & 0x7FFFFFu) == 0x7FFFFFu) got = rcp_fast(len);
+        want = 1.0f / len;
+    }
     else if (mode == 7) { got = sqrt_markstein2(x); want = __builtin_sqrtf(x); }
     else if (mode == 8) { got = sqrt_vsqrt_fma(x); want = __builtin_sqrtf(x); }
     else { got = __builtin_amdgcn_rcpf(x); want = 1.0f / x; }                            // raw v_rcp_f32
@@ -161,6 +168,7 @@ int main() {
     run("sqrt v_rsq + fma correction", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 6, 67, cnt, bad); });
     // the whole normal range 2^-126 .. 2^128 (exponents 1..254): beyond the kernel's proven callers
     run("rcp  1/RN(sqrt x) by Newton from v_rsq(x), 2^-60..2^100", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 160), dim3(256), 0, 0, 9, 67, cnt, bad); });
+    run("rcp  same + all-ones-mantissa fallback, 2^-60..2^100", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 160), dim3(256), 0, 0, 10, 67, cnt, bad); });
     run("sqrt v_rsq + fma correction, all normals", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 254), dim3(256), 0, 0, 6, 1, cnt, bad); });
     run("sqrt v_sqrt+fix, all normals", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 254), dim3(256), 0, 0, 1, 1, cnt, bad); });
     run("sqrt v_rsq + Goldschmidt + correction", [&] { hipLaunchKernelGGL(k_unary, dim3(1 << 15, 120), dim3(256), 0, 0, 7, 67, cnt, bad); });

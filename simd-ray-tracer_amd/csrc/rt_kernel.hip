@@ -88,9 +88,10 @@ __device__ __forceinline__ float rcp_rn(float b) {
 #ifndef RTK_SQRT_FIX
 #define RTK_SQRT_FIX 4
 #endif
-__device__ __forceinline__ float sqrt_rn(float x) {
+__device__ __forceinline__ float sqrt_rn(float x, float *rsq = nullptr) {
     if (RTK_SQRT_FIX == 4) {
         const float y = __builtin_fminf(__builtin_amdgcn_rsqf(x), 0x1p64f);
+        if (rsq) *rsq = y;
         const float g = x * y, h = 0.5f * y;
         return __builtin_fmaf(__builtin_fmaf(-g, g, x), h, g);
     }
@@ -129,8 +130,23 @@ __device__ __forceinline__ float2 fold_weights(uint32_t pc) {
 __device__ __forceinline__ void normalize(float &x, float &y, float &z) {
     const float l2 = dot3(x, y, z, x, y, z);
     const bool keep = l2 > kEps;
-    const float len = sqrt_rn(l2);
-    const float inv = rcp_rn(len);
+#ifndef RTK_NORM_RSQ
+#define RTK_NORM_RSQ 0
+#endif
+    float rq = 0.0f;
+    const float len = sqrt_rn(l2, RTK_NORM_RSQ ? &rq : nullptr);
+    float inv;
+    if (RTK_NORM_RSQ) {
+        // RN(1/len) by one Newton step from sqrt_rn's v_rsq_f32(l2); exact except when len's mantissa is all
+        // ones (len just under a power of two, 1/len next to a midpoint): those lanes take rcp_rn
+        inv = __builtin_fmaf(__builtin_fmaf(-len, rq, 1.0f), rq, rq);
+        if (__builtin_expect((__float_as_uint(len) & 0x7FFFFFu) == 0x7FFFFFu, 0)) {
+            asm volatile("");
+            inv = rcp_rn(len);
+        }
+    } else {
+        inv = rcp_rn(len);
+    }
     float qx = div_rn(x, len, inv), qy = div_rn(y, len, inv), qz = div_rn(z, len, inv);
     // (a zero component also takes the IEEE path: rare, and exact either way)
     const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(qx), __builtin_fabsf(qy)), __builtin_fabsf(qz));
